@@ -1,0 +1,98 @@
+"""ctypes binding of libcheb_mi355.so (the C ABI declared in include/cheb_mi355.h).
+
+The HIP library is the only compute path: if it is missing this module raises
+ImportError -- there is no CPU or PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcheb_mi355.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cheb_mi355.h")
+
+CG_OK, CG_ERR_ARG, CG_ERR_HIP, CG_ERR_UNSUPPORTED, CG_ERR_ALLOC, CG_ERR_COMM = range(6)
+CG_PATH_AUTO, CG_PATH_RESIDENT, CG_PATH_STREAM = 0, 1, 2
+PATHS = {"auto": CG_PATH_AUTO, "resident": CG_PATH_RESIDENT, "stream": CG_PATH_STREAM}
+
+
+class CGError(RuntimeError):
+    """A non-zero status from libcheb_mi355 (message from cg_last_error())."""
+
+    def __init__(self, func, code, msg):
+        super().__init__(f"{func} failed with status {code}: {msg}")
+        self.code = code
+
+
+_c_int, _c_i32, _c_i64, _c_sz = ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+_vp, _fp = ctypes.c_void_p, ctypes.c_void_p  # device pointers are passed as void*
+_ip32 = ctypes.POINTER(ctypes.c_int32)
+_fp32 = ctypes.POINTER(ctypes.c_float)
+
+_SIGNATURES = {
+    "cg_version": ([], _c_int),
+    "cg_last_error": ([], ctypes.c_char_p),
+    "cg_plan_create": ([ctypes.POINTER(_vp), _c_int, _c_i32, _c_i64, _ip32, _ip32, _fp32,
+                        _ip32, _ip32, _fp32], _c_int),
+    "cg_plan_destroy": ([_vp], _c_int),
+    "cg_plan_set_path": ([_vp, _c_int], _c_int),
+    "cg_plan_query_path": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_int)], _c_int),
+    "cg_cheb_workspace_bytes": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_sz),
+                                 ctypes.POINTER(_c_sz)], _c_int),
+    "cg_cheb_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp],
+                        _c_int),
+    "cg_cheb_backward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_sz,
+                          _vp], _c_int),
+    "cg_perm_gather": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
+    "cg_maxpool_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp], _c_int),
+    "cg_maxpool_backward": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
+    "cg_avgpool_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
+    "cg_avgpool_backward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
+    "cg_adam_update": ([_vp, _vp, _vp, _vp, _c_i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                        ctypes.c_float, _c_i32, ctypes.c_float, _vp], _c_int),
+    "cg_comm_unique_id": ([ctypes.c_char_p], _c_int),
+    "cg_comm_init": ([ctypes.POINTER(_vp), _c_int, _c_int, ctypes.c_char_p, _c_int], _c_int),
+    "cg_allreduce_sum_f32": ([_vp, _vp, _c_sz, _vp], _c_int),
+    "cg_comm_destroy": ([_vp], _c_int),
+}
+
+_lib = None
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Every function the public header declares (used by the ABI-export test)."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(cg_\w+)\s*\(", text, re.M)))
+
+
+def lib():
+    """Load (once) and return the ctypes handle.  Raises ImportError if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is not built: run `make` (or __graft_entry__.build()) -- "
+            "cnn_graph_amd has no CPU/PyTorch fallback for its HIP kernels")
+    h = ctypes.CDLL(LIB_PATH)
+    for name, (argtypes, restype) in _SIGNATURES.items():
+        fn = getattr(h, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = h
+    return h
+
+
+def check(func_name: str, status: int):
+    if status != CG_OK:
+        msg = lib().cg_last_error()
+        raise CGError(func_name, status, msg.decode() if msg else "")
+
+
+def call(func_name: str, *args):
+    """Call a C-ABI function and raise CGError on a non-zero status."""
+    status = getattr(lib(), func_name)(*args)
+    check(func_name, status)
+    return status

@@ -1,0 +1,74 @@
+// Internal declarations shared by the HIP translation units of libcheb_mi355.
+// Not part of the public ABI (that is include/cheb_mi355.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace cg {
+
+constexpr int kWave = 64;
+constexpr int kResidentThreads = 512;  // 8 waves: two per SIMD, one workgroup per CU
+constexpr int kLdsBytes = 160 * 1024;  // gfx950 LDS per CU
+
+// Padded LDS row stride for a vertex vector: >= M, == 1 (mod 32) so that the
+// 32 lanes of a half-wave writing 32 different rows at one vertex hit 32
+// different banks (ds_write_b32 banks are (addr/4) mod 32).
+__host__ __device__ inline int lds_vertex_stride(int M) { return ((M + 31) / 32) * 32 + 1; }
+__host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
+
+// ---- resident (LDS) path ---------------------------------------------------
+struct ResidentGeom {
+  int mt;          // m-tiles of 32 vertices per wave (template arg, >= needed)
+  int nt;          // 32-wide tiles over Fout (forward) (template arg)
+  size_t fwd_lds;  // dynamic LDS bytes of the forward kernel
+  size_t bwd_lds;  // dynamic LDS bytes of the backward kernel
+  bool fwd_ok;
+  bool bwd_ok;
+};
+ResidentGeom resident_geometry(int M, int64_t nnz, int64_t nnzT, int Fin, int K, int Fout);
+
+hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
+                                   int nnz, const int* rowptr, const uint16_t* col16,
+                                   const float* val, const float* x, const float* W, float* basis,
+                                   float* y, hipStream_t s);
+hipError_t launch_resident_backward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
+                                    int nnzT, const int* trowptr, const uint16_t* tcol16,
+                                    const float* tval, const float* dy, const float* basis,
+                                    const float* W, float* dx, float* dw_slab, hipStream_t s);
+
+// ---- streaming path ----------------------------------------------------------
+hipError_t launch_x_to_cols(const float* x, float* T0, float* basis, int N, int M, int Fin, int K,
+                            hipStream_t s);
+hipError_t launch_spmm_cheb_step(const int* rowptr, const int* col, const float* val,
+                                 const float* Tprev, const float* Tprev2, float* Tout, float* basis,
+                                 int N, int M, int Fin, int K, int k, hipStream_t s);
+hipError_t launch_clenshaw_step(const int* trowptr, const int* tcol, const float* tval,
+                                const float* Gn1, const float* Gn2, float* Gout, const float* dA,
+                                float* dx, int N, int M, int Fin, int K, int k, hipStream_t s);
+// C[Mg x Ng] (+)= op(A)[Mg x Kg] * op(B)[Kg x Ng]; fp32 in/out on MFMA f32.
+// trans_a: A stored [Kg][lda] (A^T row-major); trans_b: B stored [Ng][ldb].
+// splits > 1: the K range is cut into `splits` slices, slice s writes
+// C + s*Mg*ldc (a partial slab, reduced later by launch_reduce_slabs).
+hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, const float* A,
+                           int lda, const float* B, int ldb, float* C, int ldc, int splits,
+                           hipStream_t s);
+// Number of K slices launch_gemm_f32 actually uses for `splits` requested.
+int gemm_effective_splits(int Kg, int splits);
+hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,
+                               hipStream_t s);
+
+// ---- misc ----------------------------------------------------------------------
+hipError_t launch_perm_gather(const float* x, const int32_t* perm, int N, int M_in, int M_out,
+                              int F, float* out, hipStream_t s);
+hipError_t launch_maxpool_fwd(const float* x, int N, int M, int F, int p, float* y, int32_t* arg,
+                              hipStream_t s);
+hipError_t launch_maxpool_bwd(const float* dy, const int32_t* arg, int N, int M, int F, int p,
+                              float* dx, hipStream_t s);
+hipError_t launch_avgpool_fwd(const float* x, int N, int M, int F, int p, float* y, hipStream_t s);
+hipError_t launch_avgpool_bwd(const float* dy, int N, int M, int F, int p, float* dx,
+                              hipStream_t s);
+hipError_t launch_adam(float* param, const float* grad, float* m, float* v, int64_t n, float lr_t,
+                       float beta1, float beta2, float eps, float grad_scale, hipStream_t s);
+
+}  // namespace cg

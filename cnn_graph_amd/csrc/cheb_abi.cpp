@@ -1,0 +1,429 @@
+// C ABI of libcheb_mi355.so (see include/cheb_mi355.h): plan management,
+// argument validation, workspace layout and kernel-path dispatch.
+#include "../../include/cheb_mi355.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "cg_internal.h"
+
+struct cg_plan {
+  int device = 0;
+  int M = 0;
+  int64_t nnz = 0, nnzT = 0;
+  int path = CG_PATH_AUTO;
+  int* rowptr = nullptr;
+  int* col = nullptr;
+  float* val = nullptr;
+  uint16_t* col16 = nullptr;
+  int* trowptr = nullptr;
+  int* tcol = nullptr;
+  float* tval = nullptr;
+  uint16_t* tcol16 = nullptr;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int ok() {
+  g_err.clear();
+  return CG_OK;
+}
+
+#define CG_HIP(call)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess) return fail(CG_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+// Validates a host CSR: rowptr[0] = 0, non-decreasing, rowptr[M] = nnz,
+// columns in [0, M) strictly increasing inside each row (canonical order,
+// what tf.sparse_reorder produces at lib/graph_conv.py:153).
+int check_csr(const char* what, int32_t M, int64_t nnz, const int32_t* rowptr, const int32_t* col,
+              const float* val) {
+  if (!rowptr || (nnz > 0 && (!col || !val))) return fail(CG_ERR_ARG, "%s: null CSR array", what);
+  if (rowptr[0] != 0 || rowptr[M] != nnz)
+    return fail(CG_ERR_ARG, "%s: rowptr[0]=%d rowptr[M]=%d nnz=%lld", what, rowptr[0], rowptr[M],
+                (long long)nnz);
+  for (int32_t r = 0; r < M; ++r) {
+    if (rowptr[r + 1] < rowptr[r]) return fail(CG_ERR_ARG, "%s: rowptr decreases at row %d", what, r);
+    for (int32_t j = rowptr[r]; j < rowptr[r + 1]; ++j) {
+      if (col[j] < 0 || col[j] >= M)
+        return fail(CG_ERR_ARG, "%s: column %d out of range at nnz %d", what, col[j], j);
+      if (j > rowptr[r] && col[j] <= col[j - 1])
+        return fail(CG_ERR_ARG, "%s: columns not strictly increasing in row %d", what, r);
+    }
+  }
+  return CG_OK;
+}
+
+// Exact transpose (counting sort by column; rows come out in increasing order,
+// so columns of the transpose are sorted).
+void transpose_csr(int32_t M, int64_t nnz, const int32_t* rp, const int32_t* ci, const float* v,
+                   std::vector<int32_t>& trp, std::vector<int32_t>& tci, std::vector<float>& tv) {
+  trp.assign(size_t(M) + 1, 0);
+  tci.resize(size_t(nnz));
+  tv.resize(size_t(nnz));
+  for (int64_t j = 0; j < nnz; ++j) trp[size_t(ci[j]) + 1]++;
+  for (int32_t r = 0; r < M; ++r) trp[size_t(r) + 1] += trp[size_t(r)];
+  std::vector<int32_t> fill(trp.begin(), trp.end() - 1);
+  for (int32_t r = 0; r < M; ++r)
+    for (int32_t j = rp[r]; j < rp[r + 1]; ++j) {
+      const int32_t dst = fill[size_t(ci[j])]++;
+      tci[size_t(dst)] = r;
+      tv[size_t(dst)] = v[j];
+    }
+}
+
+template <typename T>
+int upload(T** dst, const T* src, size_t count) {
+  *dst = nullptr;
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  CG_HIP(hipMalloc(reinterpret_cast<void**>(dst), bytes));
+  if (count) CG_HIP(hipMemcpy(*dst, src, count * sizeof(T), hipMemcpyHostToDevice));
+  return CG_OK;
+}
+
+void free_plan(cg_plan* p) {
+  if (!p) return;
+  void* ptrs[] = {p->rowptr, p->col, p->val, p->col16, p->trowptr, p->tcol, p->tval, p->tcol16};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  delete p;
+}
+
+int check_device(const cg_plan* p) {
+  int d = -1;
+  CG_HIP(hipGetDevice(&d));
+  if (d != p->device)
+    return fail(CG_ERR_ARG, "current HIP device %d differs from the plan's device %d", d,
+                p->device);
+  return CG_OK;
+}
+
+int check_shape(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout) {
+  if (!p) return fail(CG_ERR_ARG, "null plan");
+  if (N < 1 || Fin < 1 || K < 1 || Fout < 1)
+    return fail(CG_ERR_ARG, "bad shape N=%d Fin=%d K=%d Fout=%d", N, Fin, K, Fout);
+  if (int64_t(N) * p->M >= (int64_t(1) << 31) || int64_t(N) * Fin >= (int64_t(1) << 31))
+    return fail(CG_ERR_ARG, "N*M or N*Fin exceeds 2^31");
+  return CG_OK;
+}
+
+int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool backward,
+                int* path) {
+  const cg::ResidentGeom g = cg::resident_geometry(p->M, p->nnz, p->nnzT, Fin, K, Fout);
+  const bool fits = backward ? g.bwd_ok : g.fwd_ok;
+  if (p->path == CG_PATH_STREAM) {
+    *path = CG_PATH_STREAM;
+  } else if (p->path == CG_PATH_RESIDENT) {
+    if (!fits)
+      return fail(CG_ERR_UNSUPPORTED,
+                  "resident path does not fit: M=%d nnz=%lld Fin=%d K=%d Fout=%d (lds fwd %zu / "
+                  "bwd %zu bytes)",
+                  p->M, (long long)p->nnz, Fin, K, Fout, g.fwd_lds, g.bwd_lds);
+    *path = CG_PATH_RESIDENT;
+  } else {
+    *path = fits ? CG_PATH_RESIDENT : CG_PATH_STREAM;
+  }
+  return CG_OK;
+}
+
+inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
+
+int dw_splits(int64_t NM, int FinK, int Fout) {
+  const int64_t tiles = int64_t((FinK + 63) / 64) * ((Fout + 63) / 64);
+  int64_t s = std::max<int64_t>(1, 1024 / std::max<int64_t>(tiles, 1));
+  s = std::min<int64_t>(s, std::max<int64_t>(1, NM / 256));
+  return int(s);
+}
+
+struct StreamWs {
+  size_t ring;   // 3 * M * B floats
+  size_t dA;     // N*M*FinK floats
+  size_t slabs;  // S * FinK * Fout floats
+  int S;
+};
+
+StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout) {
+  StreamWs w{};
+  const int64_t B = int64_t(N) * Fin;
+  const int64_t FinK = int64_t(Fin) * K;
+  const int64_t NM = int64_t(N) * p->M;
+  w.ring = al256(size_t(3) * size_t(p->M) * size_t(B) * 4);
+  w.dA = al256(size_t(NM) * size_t(FinK) * 4);
+  w.S = cg::gemm_effective_splits(int(NM), dw_splits(NM, int(FinK), Fout));
+  w.slabs = al256(size_t(w.S) * size_t(FinK) * size_t(Fout) * 4);
+  return w;
+}
+
+int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                    size_t* fwd, size_t* bwd) {
+  int pf = 0, pb = 0, rc;
+  if ((rc = choose_path(p, Fin, K, Fout, false, &pf))) return rc;
+  if ((rc = choose_path(p, Fin, K, Fout, true, &pb))) return rc;
+  const StreamWs w = stream_ws(p, N, Fin, K, Fout);
+  *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.ring;
+  *bwd = (pb == CG_PATH_RESIDENT) ? al256(size_t(N) * size_t(Fin) * K * Fout * 4)
+                                  : (w.ring + w.dA + w.slabs);
+  return CG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cg_version(void) { return 100; }
+
+// Not in the public header: lets comm.cpp report through cg_last_error().
+int cg_internal_set_error(int code, const char* msg) {
+  if (code == CG_OK) return ok();
+  return fail(code, "%s", msg ? msg : "");
+}
+
+const char* cg_last_error(void) { return g_err.c_str(); }
+
+int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz, const int32_t* rowptr,
+                   const int32_t* col, const float* val, const int32_t* t_rowptr,
+                   const int32_t* t_col, const float* t_val) {
+  if (!plan) return fail(CG_ERR_ARG, "null plan out-pointer");
+  *plan = nullptr;
+  if (M < 1 || nnz < 0 || nnz >= (int64_t(1) << 31))
+    return fail(CG_ERR_ARG, "bad M=%d nnz=%lld", M, (long long)nnz);
+  int rc = check_csr("L", M, nnz, rowptr, col, val);
+  if (rc) return rc;
+  std::vector<int32_t> trp, tci;
+  std::vector<float> tv;
+  if (t_rowptr) {
+    const int64_t nnzT = t_rowptr[M];
+    if (nnzT != nnz) return fail(CG_ERR_ARG, "transpose nnz %lld != nnz %lld", (long long)nnzT,
+                                 (long long)nnz);
+    if ((rc = check_csr("L^T", M, nnz, t_rowptr, t_col, t_val))) return rc;
+    trp.assign(t_rowptr, t_rowptr + M + 1);
+    tci.assign(t_col, t_col + nnz);
+    tv.assign(t_val, t_val + nnz);
+  } else {
+    transpose_csr(M, nnz, rowptr, col, val, trp, tci, tv);
+  }
+
+  int prev = 0;
+  CG_HIP(hipGetDevice(&prev));
+  CG_HIP(hipSetDevice(device));
+  cg_plan* p = new (std::nothrow) cg_plan();
+  if (!p) return fail(CG_ERR_ALLOC, "out of host memory");
+  p->device = device;
+  p->M = M;
+  p->nnz = nnz;
+  p->nnzT = nnz;
+  rc = upload(&p->rowptr, rowptr, size_t(M) + 1);
+  if (!rc) rc = upload(&p->col, col, size_t(nnz));
+  if (!rc) rc = upload(&p->val, val, size_t(nnz));
+  if (!rc) rc = upload(&p->trowptr, trp.data(), trp.size());
+  if (!rc) rc = upload(&p->tcol, tci.data(), tci.size());
+  if (!rc) rc = upload(&p->tval, tv.data(), tv.size());
+  if (!rc && M <= 65535) {
+    std::vector<uint16_t> c16(col, col + nnz), t16(tci.begin(), tci.end());
+    rc = upload(&p->col16, c16.data(), c16.size());
+    if (!rc) rc = upload(&p->tcol16, t16.data(), t16.size());
+  }
+  (void)hipSetDevice(prev);
+  if (rc) {
+    free_plan(p);
+    return rc;
+  }
+  *plan = p;
+  return ok();
+}
+
+int cg_plan_destroy(cg_plan* plan) {
+  free_plan(plan);
+  return ok();
+}
+
+int cg_plan_set_path(cg_plan* plan, int path) {
+  if (!plan) return fail(CG_ERR_ARG, "null plan");
+  if (path != CG_PATH_AUTO && path != CG_PATH_RESIDENT && path != CG_PATH_STREAM)
+    return fail(CG_ERR_ARG, "bad path %d", path);
+  plan->path = path;
+  return ok();
+}
+
+int cg_plan_query_path(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                       int* path) {
+  int rc = check_shape(plan, N, Fin, K, Fout);
+  if (rc) return rc;
+  if (!path) return fail(CG_ERR_ARG, "null path out-pointer");
+  if ((rc = choose_path(plan, Fin, K, Fout, false, path))) return rc;
+  return ok();
+}
+
+int cg_cheb_workspace_bytes(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                            size_t* fwd_bytes, size_t* bwd_bytes) {
+  int rc = check_shape(plan, N, Fin, K, Fout);
+  if (rc) return rc;
+  size_t f = 0, b = 0;
+  if ((rc = workspace_bytes(plan, N, Fin, K, Fout, &f, &b))) return rc;
+  if (fwd_bytes) *fwd_bytes = f;
+  if (bwd_bytes) *bwd_bytes = b;
+  return ok();
+}
+
+int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                    const float* x, const float* W, float* basis, float* y, void* workspace,
+                    size_t ws_bytes, void* stream) {
+  int rc = check_shape(plan, N, Fin, K, Fout);
+  if (rc) return rc;
+  if (!x) return fail(CG_ERR_ARG, "null x");
+  if (y && !W) return fail(CG_ERR_ARG, "null W with non-null y");
+  if (!y && !basis) return fail(CG_ERR_ARG, "nothing to compute (basis and y both null)");
+  if ((rc = check_device(plan))) return rc;
+  int path = 0;
+  if ((rc = choose_path(plan, Fin, K, Fout, false, &path))) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int M = plan->M;
+
+  if (path == CG_PATH_RESIDENT) {
+    const cg::ResidentGeom g = cg::resident_geometry(M, plan->nnz, plan->nnzT, Fin, K, Fout);
+    CG_HIP(cg::launch_resident_forward(g, N, M, Fin, K, Fout, int(plan->nnz), plan->rowptr,
+                                       plan->col16, plan->val, x, y ? W : nullptr, basis, y, s));
+    return ok();
+  }
+  // streaming path
+  if (!basis) return fail(CG_ERR_ARG, "streaming path needs a basis buffer (the GEMM reads it)");
+  const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
+  if (!workspace || ws_bytes < w.ring)
+    return fail(CG_ERR_ARG, "forward workspace too small: %zu < %zu", ws_bytes, w.ring);
+  float* ring = static_cast<float*>(workspace);
+  const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
+  auto T = [&](int k) { return ring + size_t(k % 3) * slot; };
+  CG_HIP(cg::launch_x_to_cols(x, T(0), basis, N, M, Fin, K, s));
+  for (int k = 1; k < K; ++k)
+    CG_HIP(cg::launch_spmm_cheb_step(plan->rowptr, plan->col, plan->val, T(k - 1),
+                                     k >= 2 ? T(k - 2) : nullptr, (k < K - 1) ? T(k) : nullptr,
+                                     basis, N, M, Fin, K, k, s));
+  if (y)
+    CG_HIP(cg::launch_gemm_f32(false, false, N * M, Fout, Fin * K, basis, Fin * K, W, Fout, y,
+                               Fout, 1, s));
+  return ok();
+}
+
+int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                     const float* dy, const float* basis, const float* W, float* dx, float* dW,
+                     void* workspace, size_t ws_bytes, void* stream) {
+  int rc = check_shape(plan, N, Fin, K, Fout);
+  if (rc) return rc;
+  if (!dy || !basis || !W || !dW) return fail(CG_ERR_ARG, "null dy/basis/W/dW");
+  if ((rc = check_device(plan))) return rc;
+  int path = 0;
+  if ((rc = choose_path(plan, Fin, K, Fout, true, &path))) return rc;
+  size_t need_f = 0, need_b = 0;
+  if ((rc = workspace_bytes(plan, N, Fin, K, Fout, &need_f, &need_b))) return rc;
+  if (!workspace || ws_bytes < need_b)
+    return fail(CG_ERR_ARG, "backward workspace too small: %zu < %zu", ws_bytes, need_b);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int M = plan->M;
+  const int FinK = Fin * K;
+
+  if (path == CG_PATH_RESIDENT) {
+    const cg::ResidentGeom g = cg::resident_geometry(M, plan->nnz, plan->nnzT, Fin, K, Fout);
+    float* slab = static_cast<float*>(workspace);
+    CG_HIP(cg::launch_resident_backward(g, N, M, Fin, K, Fout, int(plan->nnzT), plan->trowptr,
+                                        plan->tcol16, plan->tval, dy, basis, W, dx, slab, s));
+    CG_HIP(cg::launch_reduce_slabs(slab, N, int64_t(FinK) * Fout, dW, s));
+    return ok();
+  }
+  const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
+  char* base = static_cast<char*>(workspace);
+  float* ring = reinterpret_cast<float*>(base);
+  float* dA = reinterpret_cast<float*>(base + w.ring);
+  float* slabs = reinterpret_cast<float*>(base + w.ring + w.dA);
+  const int NM = N * M;
+  // dW = basis^T dy  (split over N*M, fixed-order slab reduction -> deterministic)
+  CG_HIP(cg::launch_gemm_f32(true, false, FinK, Fout, NM, basis, FinK, dy, Fout, slabs, Fout,
+                             dw_splits(NM, FinK, Fout), s));
+  CG_HIP(cg::launch_reduce_slabs(slabs, w.S, int64_t(FinK) * Fout, dW, s));
+  if (!dx) return ok();
+  // dBasis = dy W^T
+  CG_HIP(cg::launch_gemm_f32(false, true, NM, FinK, Fout, dy, Fout, W, Fout, dA, FinK, 1, s));
+  const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
+  auto G = [&](int k) { return ring + size_t(k % 3) * slot; };
+  for (int k = K - 1; k >= 0; --k)
+    CG_HIP(cg::launch_clenshaw_step(plan->trowptr, plan->tcol, plan->tval, G(k + 1), G(k + 2),
+                                    G(k), dA, dx, N, M, Fin, K, k, s));
+  return ok();
+}
+
+int cg_perm_gather(const float* x, const int32_t* perm, int32_t N, int32_t M_in, int32_t M_out,
+                   int32_t F, float* out, void* stream) {
+  if (!x || !perm || !out || N < 1 || M_in < 1 || M_out < 1 || F < 1)
+    return fail(CG_ERR_ARG, "perm_gather: bad arguments");
+  CG_HIP(cg::launch_perm_gather(x, perm, N, M_in, M_out, F, out,
+                                reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_maxpool_forward(const float* x, int32_t N, int32_t M, int32_t F, int32_t p, float* y,
+                       int32_t* argmax, void* stream) {
+  if (!x || !y || N < 1 || M < 1 || F < 1 || p < 1 || M % p)
+    return fail(CG_ERR_ARG, "maxpool_forward: bad arguments (M=%d p=%d)", M, p);
+  CG_HIP(cg::launch_maxpool_fwd(x, N, M, F, p, y, argmax, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_maxpool_backward(const float* dy, const int32_t* argmax, int32_t N, int32_t M, int32_t F,
+                        int32_t p, float* dx, void* stream) {
+  if (!dy || !argmax || !dx || N < 1 || M < 1 || F < 1 || p < 1 || M % p)
+    return fail(CG_ERR_ARG, "maxpool_backward: bad arguments (M=%d p=%d)", M, p);
+  CG_HIP(cg::launch_maxpool_bwd(dy, argmax, N, M, F, p, dx, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_avgpool_forward(const float* x, int32_t N, int32_t M, int32_t F, int32_t p, float* y,
+                       void* stream) {
+  if (!x || !y || N < 1 || M < 1 || F < 1 || p < 1 || M % p)
+    return fail(CG_ERR_ARG, "avgpool_forward: bad arguments (M=%d p=%d)", M, p);
+  CG_HIP(cg::launch_avgpool_fwd(x, N, M, F, p, y, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_avgpool_backward(const float* dy, int32_t N, int32_t M, int32_t F, int32_t p, float* dx,
+                        void* stream) {
+  if (!dy || !dx || N < 1 || M < 1 || F < 1 || p < 1 || M % p)
+    return fail(CG_ERR_ARG, "avgpool_backward: bad arguments (M=%d p=%d)", M, p);
+  CG_HIP(cg::launch_avgpool_bwd(dy, N, M, F, p, dx, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_adam_update(float* param, const float* grad, float* m, float* v, int64_t n, float lr,
+                   float beta1, float beta2, float eps, int32_t step, float grad_scale,
+                   void* stream) {
+  if (!param || !grad || !m || !v || n < 0 || step < 1)
+    return fail(CG_ERR_ARG, "adam_update: bad arguments");
+  if (n == 0) return ok();
+  const double lr_t =
+      double(lr) * std::sqrt(1.0 - std::pow(double(beta2), step)) / (1.0 - std::pow(double(beta1), step));
+  CG_HIP(cg::launch_adam(param, grad, m, v, n, float(lr_t), beta1, beta2, eps, grad_scale,
+                         reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+// Ops either side of the Chebyshev filter on gfx950:
+//   perm_gather  -- lib/coarsening.py:219-240 perm_data (fake vertices -> 0)
+//   maxpool      -- lib/graph_conv.py:201-209 mpool1 (+ first-max argmax, scatter-free grad)
+//   avgpool      -- lib/graph_conv.py:211-218 apool1
+//   adam         -- lib/graph_model.py:293-298 (TF-1.x AdamOptimizer update rule)
+// All are HBM-streaming, one thread per output element, F (the feature axis,
+// contiguous in memory) on consecutive lanes so loads and stores coalesce.
+#include "cg_internal.h"
+
+namespace cg {
+namespace {
+
+inline int grid_for(int64_t total, int block) {
+  int64_t g = (total + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return int(g);
+}
+
+__global__ __launch_bounds__(256) void k_perm_gather(const float* __restrict__ x,
+                                                     const int32_t* __restrict__ perm, int N,
+                                                     int M_in, int M_out, int F,
+                                                     float* __restrict__ out) {
+  const int64_t total = int64_t(N) * M_out * F;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t f = i % F;
+    const int64_t t = i / F;
+    const int64_t v = t % M_out, n = t / M_out;
+    const int src = perm[v];
+    out[i] = (src >= 0 && src < M_in) ? x[(n * M_in + src) * F + f] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_maxpool_fwd(const float* __restrict__ x, int N, int M,
+                                                     int F, int p, float* __restrict__ y,
+                                                     int32_t* __restrict__ arg) {
+  const int Mo = M / p;
+  const int64_t total = int64_t(N) * Mo * F;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t f = i % F;
+    const int64_t t = i / F;
+    const int64_t o = t % Mo, n = t / Mo;
+    const float* base = x + (n * M + o * p) * F + f;
+    float best = base[0];
+    int bi = 0;
+    for (int j = 1; j < p; ++j) {
+      const float v = base[int64_t(j) * F];
+      if (best < v) {  // strict: the first maximum in window order wins
+        best = v;
+        bi = j;
+      }
+    }
+    y[i] = best;
+    if (arg) arg[i] = int32_t(o * p + bi);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_maxpool_bwd(const float* __restrict__ dy,
+                                                     const int32_t* __restrict__ arg, int N, int M,
+                                                     int F, int p, float* __restrict__ dx) {
+  const int Mo = M / p;
+  const int64_t total = int64_t(N) * M * F;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t f = i % F;
+    const int64_t t = i / F;
+    const int64_t m = t % M, n = t / M;
+    const int64_t o = m / p;
+    const int64_t oi = (n * Mo + o) * F + f;
+    dx[i] = (arg[oi] == m) ? dy[oi] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_avgpool_fwd(const float* __restrict__ x, int N, int M,
+                                                     int F, int p, float* __restrict__ y) {
+#pragma clang fp contract(off)
+  const int Mo = M / p;
+  const int64_t total = int64_t(N) * Mo * F;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t f = i % F;
+    const int64_t t = i / F;
+    const int64_t o = t % Mo, n = t / Mo;
+    const float* base = x + (n * M + o * p) * F + f;
+    float s = 0.f;
+    for (int j = 0; j < p; ++j) s = s + base[int64_t(j) * F];
+    y[i] = s / float(p);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_avgpool_bwd(const float* __restrict__ dy, int N, int M,
+                                                     int F, int p, float* __restrict__ dx) {
+  const int Mo = M / p;
+  const int64_t total = int64_t(N) * M * F;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t f = i % F;
+    const int64_t t = i / F;
+    const int64_t m = t % M, n = t / M;
+    dx[i] = dy[(n * Mo + m / p) * F + f] / float(p);
+  }
+}
+
+// m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ; p -= lr_t m / (sqrt(v) + eps)
+// with lr_t = lr sqrt(1-b2^t)/(1-b1^t) computed on the host (TF's ApplyAdam).
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ param,
+                                              const float* __restrict__ grad, float* __restrict__ m,
+                                              float* __restrict__ v, int64_t n, float lr_t,
+                                              float beta1, float beta2, float eps,
+                                              float grad_scale) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const float g = grad[i] * grad_scale;
+    const float mi = m[i] + (g - m[i]) * (1.f - beta1);
+    const float vi = v[i] + (g * g - v[i]) * (1.f - beta2);
+    m[i] = mi;
+    v[i] = vi;
+    param[i] = param[i] - lr_t * mi / (sqrtf(vi) + eps);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_perm_gather(const float* x, const int32_t* perm, int N, int M_in, int M_out,
+                              int F, float* out, hipStream_t s) {
+  const int64_t total = int64_t(N) * M_out * F;
+  hipLaunchKernelGGL(k_perm_gather, dim3(grid_for(total, 256)), dim3(256), 0, s, x, perm, N, M_in,
+                     M_out, F, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_maxpool_fwd(const float* x, int N, int M, int F, int p, float* y, int32_t* arg,
+                              hipStream_t s) {
+  const int64_t total = int64_t(N) * (M / p) * F;
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_for(total, 256)), dim3(256), 0, s, x, N, M, F, p, y,
+                     arg);
+  return hipGetLastError();
+}
+
+hipError_t launch_maxpool_bwd(const float* dy, const int32_t* arg, int N, int M, int F, int p,
+                              float* dx, hipStream_t s) {
+  const int64_t total = int64_t(N) * M * F;
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(total, 256)), dim3(256), 0, s, dy, arg, N, M, F,
+                     p, dx);
+  return hipGetLastError();
+}
+
+hipError_t launch_avgpool_fwd(const float* x, int N, int M, int F, int p, float* y,
+                              hipStream_t s) {
+  const int64_t total = int64_t(N) * (M / p) * F;
+  hipLaunchKernelGGL(k_avgpool_fwd, dim3(grid_for(total, 256)), dim3(256), 0, s, x, N, M, F, p, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_avgpool_bwd(const float* dy, int N, int M, int F, int p, float* dx,
+                              hipStream_t s) {
+  const int64_t total = int64_t(N) * M * F;
+  hipLaunchKernelGGL(k_avgpool_bwd, dim3(grid_for(total, 256)), dim3(256), 0, s, dy, N, M, F, p,
+                     dx);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam(float* param, const float* grad, float* m, float* v, int64_t n, float lr_t,
+                       float beta1, float beta2, float eps, float grad_scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_adam, dim3(grid_for(n, 256)), dim3(256), 0, s, param, grad, m, v, n, lr_t,
+                     beta1, beta2, eps, grad_scale);
+  return hipGetLastError();
+}
+
+}  // namespace cg

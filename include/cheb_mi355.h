@@ -1,0 +1,150 @@
+/*
+ * cheb_mi355.h -- C ABI of libcheb_mi355.so, the MI355X (gfx950) Chebyshev
+ * spectral graph-convolution path.
+ *
+ * Drop-in boundary for the reference's filter plug-in
+ *   lib/graph_conv.py:144-176  GraphConv.chebyshev5(x, L, Fout, K)
+ *   lib/models.py:192-224      cgcnn.chebyshev5 (identical copy)
+ *   lib/filter.py:45-95        cheby_conv(x, L, lmax, feat_out, K, W)
+ * plus the ops adjacent to it on the path:
+ *   lib/graph_conv.py:201-218  mpool1 / apool1
+ *   lib/coarsening.py:219-240  perm_data
+ *   lib/graph_model.py:293-298 Adam (compute_gradients -> apply_gradients),
+ *                              with the data-parallel all-reduce inserted between.
+ *
+ * Conventions
+ *   - Every function returns int status (CG_OK == 0); on failure
+ *     cg_last_error() returns a thread-local message.  No C++ exception
+ *     crosses the ABI.
+ *   - Tensor pointers are DEVICE pointers owned by the caller (e.g. a torch
+ *     tensor's data_ptr()), fp32, dense row-major, 16-byte aligned.
+ *   - Calls are asynchronous on the given hipStream_t (passed as void*;
+ *     NULL = the legacy default stream).  No call allocates or synchronises
+ *     inside the compute entry points, so they may be captured in a hipGraph.
+ *   - A plan is not thread-safe; use one process per GPU.
+ *   - Shapes use the reference's names: N samples, M vertices, Fin / Fout
+ *     features, K Chebyshev order.
+ */
+#ifndef CHEB_MI355_H
+#define CHEB_MI355_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  CG_OK = 0,
+  CG_ERR_ARG = 1,          /* bad shape / null pointer / inconsistent CSR          */
+  CG_ERR_HIP = 2,          /* a HIP runtime call failed                            */
+  CG_ERR_UNSUPPORTED = 3,  /* shape not supported by the requested kernel path     */
+  CG_ERR_ALLOC = 4,        /* device allocation failed                             */
+  CG_ERR_COMM = 5          /* RCCL failure                                         */
+};
+
+/* Kernel path selection for cg_plan_set_path (default CG_PATH_AUTO). */
+enum {
+  CG_PATH_AUTO = 0,     /* resident path when it fits, streaming otherwise          */
+  CG_PATH_RESIDENT = 1, /* one workgroup per sample, whole recurrence in LDS        */
+  CG_PATH_STREAM = 2    /* one launch per Chebyshev step + MFMA GEMMs (any size)    */
+};
+
+typedef struct cg_plan cg_plan;
+typedef struct cg_comm cg_comm;
+
+/* ABI version (major*10000 + minor*100 + patch). */
+int cg_version(void);
+/* Message for the last non-zero status on this thread ("" if none). */
+const char* cg_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Plan: the rescaled Laplacian L~ = L/(lmax/2) - I as host CSR (int32 row
+ * pointers / column indices sorted within each row, i.e. the row-major order
+ * tf.sparse_reorder gives at lib/graph_conv.py:153; fp32 values), copied to
+ * the device once -- the analogue of the TF graph constant built at
+ * lib/graph_conv.py:148-153.  L~^T is needed by the backward (adjoint_a SpMM);
+ * pass NULL for t_* to have it built on the host inside the call (L~ is not
+ * bit-symmetric in fp32, so it is transposed exactly, never assumed symmetric).
+ * ------------------------------------------------------------------------- */
+int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz,
+                   const int32_t* rowptr, const int32_t* col, const float* val,
+                   const int32_t* t_rowptr, const int32_t* t_col, const float* t_val);
+int cg_plan_destroy(cg_plan* plan);
+int cg_plan_set_path(cg_plan* plan, int path);
+/* Which path cg_cheb_forward/backward would take for this shape (CG_PATH_*). */
+int cg_plan_query_path(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                       int* path);
+
+/* Device workspace the forward / backward need for this shape (bytes; may be 0). */
+int cg_cheb_workspace_bytes(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                            size_t* fwd_bytes, size_t* bwd_bytes);
+
+/* ---------------------------------------------------------------------------
+ * Forward of chebyshev5 / cheby_conv (lib/graph_conv.py:155-176):
+ *   x     [N][M][Fin]            input signals
+ *   W     [Fin*K][Fout]          filter weights, row index fin*K + k (:174)
+ *   basis [N*M][Fin*K]           OUT: Chebyshev basis in the layout of :172
+ *                                (column fin*K + k); saved for the backward.
+ *                                Bit-exact to the reference's fp32 recurrence.
+ *   y     [N][M][Fout]           OUT: basis @ W (:175-176); NULL => basis only
+ *                                (chebyshev2 / lib/graph.py::chebyshev analogue)
+ * ------------------------------------------------------------------------- */
+int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                    const float* x, const float* W, float* basis, float* y,
+                    void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward (TF autodiff of the above via lib/graph_model.py:296):
+ *   dy [N][M][Fout], basis (from forward), W  ->
+ *   dx [N][M][Fin]  (NULL to skip), dW [Fin*K][Fout]  (overwritten, not accumulated)
+ * dW = basis^T dy ; dBasis = dy W^T ; reverse recurrence over L~^T.
+ * ------------------------------------------------------------------------- */
+int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                     const float* dy, const float* basis, const float* W,
+                     float* dx, float* dW, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * perm_data (lib/coarsening.py:219-240) on device:
+ *   out[n][i][f] = perm[i] < M_in ? x[n][perm[i]][f] : 0   (fake vertices are 0)
+ * x [N][M_in][F], perm [M_out] (int32), out [N][M_out][F].
+ * ------------------------------------------------------------------------- */
+int cg_perm_gather(const float* x, const int32_t* perm, int32_t N, int32_t M_in, int32_t M_out,
+                   int32_t F, float* out, void* stream);
+
+/* mpool1 (lib/graph_conv.py:201-209): window = stride = p along vertices,
+ * y [N][M/p][F]; argmax [N][M/p][F] = absolute vertex index of the FIRST
+ * maximum in window order (TF-1.x CPU MaxPoolGrad tie rule). M % p == 0. */
+int cg_maxpool_forward(const float* x, int32_t N, int32_t M, int32_t F, int32_t p,
+                       float* y, int32_t* argmax, void* stream);
+/* dx [N][M][F] = dy routed to argmax, 0 elsewhere (fully overwritten). */
+int cg_maxpool_backward(const float* dy, const int32_t* argmax, int32_t N, int32_t M, int32_t F,
+                        int32_t p, float* dx, void* stream);
+/* apool1 (lib/graph_conv.py:211-218) and its gradient. */
+int cg_avgpool_forward(const float* x, int32_t N, int32_t M, int32_t F, int32_t p, float* y,
+                       void* stream);
+int cg_avgpool_backward(const float* dy, int32_t N, int32_t M, int32_t F, int32_t p, float* dx,
+                        void* stream);
+
+/* TF-1.x Adam update (lib/graph_model.py:293-298) on n fp32 parameters;
+ * grad is multiplied by grad_scale first (1/world_size after an all-reduce
+ * SUM).  step is 1-based. */
+int cg_adam_update(float* param, const float* grad, float* m, float* v, int64_t n, float lr,
+                   float beta1, float beta2, float eps, int32_t step, float grad_scale,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Data-parallel gradient exchange over RCCL (xGMI), for callers that do not
+ * use torch.distributed.  One communicator per process/GPU; the unique id is
+ * created on rank 0 and shipped by the caller (file, socket, store).
+ * ------------------------------------------------------------------------- */
+int cg_comm_unique_id(unsigned char id[128]);
+int cg_comm_init(cg_comm** comm, int nranks, int rank, const unsigned char id[128], int device);
+int cg_allreduce_sum_f32(cg_comm* comm, float* buf, size_t count, void* stream);
+int cg_comm_destroy(cg_comm* comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CHEB_MI355_H */

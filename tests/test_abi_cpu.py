@@ -1,0 +1,55 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the
+public header declares, and rejects bad arguments before touching the device."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from cnn_graph_amd import _lib
+
+
+def test_library_exports_every_header_symbol(built_lib):
+    h = _lib.lib()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 19
+    missing = [s for s in syms if not hasattr(h, s)]
+    assert missing == []
+    assert set(syms) == set(_lib._SIGNATURES), "ctypes signatures out of sync with the header"
+
+
+def test_version(built_lib):
+    assert _lib.lib().cg_version() == 100
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32).ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32).ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+@pytest.mark.parametrize("rowptr,col,msg", [
+    ([0, 2, 3], [1, 0, 0], "not strictly increasing"),   # unsorted row 0
+    ([0, 1, 2], [0, 5], "out of range"),                   # column >= M
+    ([0, 2, 1], [0, 1], "rowptr"),                         # rowptr[M] != nnz / decreasing
+])
+def test_plan_create_rejects_bad_csr(built_lib, rowptr, col, msg):
+    h = _lib.lib()
+    rp, ci = np.array(rowptr, np.int32), np.array(col, np.int32)
+    val = np.ones(len(ci), np.float32)
+    out = ctypes.c_void_p()
+    st = h.cg_plan_create(ctypes.byref(out), 0, 2, len(ci), _i32(rp), _i32(ci), _f32(val), None, None, None)
+    assert st == _lib.CG_ERR_ARG
+    assert msg in h.cg_last_error().decode()
+    assert not out.value
+
+
+def test_null_and_shape_errors(built_lib):
+    h = _lib.lib()
+    assert h.cg_plan_set_path(None, 0) == _lib.CG_ERR_ARG
+    assert h.cg_cheb_forward(None, 1, 1, 1, 1, None, None, None, None, None, 0, None) == _lib.CG_ERR_ARG
+    assert h.cg_maxpool_forward(None, 1, 6, 1, 4, None, None, None) == _lib.CG_ERR_ARG
+    assert h.cg_adam_update(None, None, None, None, 1, 0.1, 0.9, 0.999, 1e-8, 0, 1.0, None) == _lib.CG_ERR_ARG
+    with pytest.raises(_lib.CGError):
+        _lib.call("cg_plan_set_path", None, 0)

@@ -1,0 +1,190 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the golden
+fixtures.  Bars: the Chebyshev basis is BIT-EXACT to the reference's fp32
+recurrence (lib/graph.py::chebyshev); y / dx / dW within 1e-5
+max-abs-normalised of the float64 truth; pooling values and indices exact."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse
+
+from conftest import CASES, CASE_IDS, case, load_golden
+from oracle import cheb_oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def dev(built_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_graph_amd import _lib
+    _lib.lib()
+    return torch.device("cuda", 0)
+
+
+def make_plan(c, path):
+    from cnn_graph_amd.plan import ChebPlan
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    return ChebPlan(Lt, device=0, path=path)
+
+
+def t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def test_native_library_is_the_in_tree_build(dev):
+    from cnn_graph_amd import _lib
+    assert os.path.dirname(_lib.LIB_PATH).endswith("cnn_graph_amd")
+    with open("/proc/self/maps") as f:
+        assert any("libcheb_mi355.so" in line for line in f)
+
+
+@pytest.mark.parametrize("path", ["resident", "stream"])
+@pytest.mark.parametrize("fname,prefix", CASES, ids=CASE_IDS)
+def test_forward_backward_golden(dev, fname, prefix, path):
+    from cnn_graph_amd import ops
+    c = case(load_golden(fname), prefix)
+    plan = make_plan(c, path)
+    assert plan.query_path(c["N"], c["Fin"], c["K"], c["Fout"]) == path
+    x, W, dy = t(c["x"], dev), t(c["W"], dev), t(c["dy"], dev)
+    basis, y = ops.cheb_forward(plan, x, W, c["K"])
+    torch.cuda.synchronize()
+    assert np.array_equal(basis.cpu().numpy(), c["basis"]), "basis not bit-exact"
+    assert O.normwise_err(y.cpu().numpy(), c["y_ref"]) < TOL
+    dx, dW = ops.cheb_backward(plan, dy, basis, W, c["K"])
+    torch.cuda.synchronize()
+    assert O.normwise_err(dx.cpu().numpy(), c["dx_ref"]) < TOL
+    assert O.normwise_err(dW.cpu().numpy(), c["dW_ref"]) < TOL
+
+
+@pytest.mark.parametrize("path", ["resident", "stream"])
+def test_config_b_full_batch_vs_oracle(dev, path):
+    """BASELINE config B at full size (N=256, M=976, K=25, Fout=32)."""
+    from cnn_graph_amd import ops
+    g = load_golden("golden_B.npz")
+    c = case(g)
+    rng = np.random.default_rng(99)
+    N = 256
+    x = rng.random((N, c["M"], 1), dtype=np.float32)
+    x[:, g["fake_rows"], :] = 0
+    W = c["W"]
+    dy = rng.standard_normal((N, c["M"], c["Fout"])).astype(np.float32)
+    plan = make_plan(c, path)
+    basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), c["K"])
+    dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), c["K"])
+    torch.cuda.synchronize()
+    ob, oy = O.cheb_forward(x, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], W, c["K"])
+    assert np.array_equal(basis.cpu().numpy(), ob)
+    assert O.normwise_err(y.cpu().numpy(), oy) < TOL
+    odx, odW = O.cheb_backward(dy, ob, W, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], N, c["M"], 1, c["K"])
+    assert O.normwise_err(dx.cpu().numpy(), odx) < TOL
+    assert O.normwise_err(dW.cpu().numpy(), odW) < TOL
+
+
+def test_resident_and_stream_agree_and_are_deterministic(dev):
+    from cnn_graph_amd import ops
+    c = case(load_golden("golden_E.npz"))
+    outs = []
+    for path in ("resident", "resident", "stream"):
+        plan = make_plan(c, path)
+        x, W, dy = t(c["x"], dev), t(c["W"], dev), t(c["dy"], dev)
+        basis, y = ops.cheb_forward(plan, x, W, c["K"])
+        dx, dW = ops.cheb_backward(plan, dy, basis, W, c["K"])
+        outs.append([a.cpu().numpy() for a in (basis, y, dx, dW)])
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b), "resident path not bitwise reproducible"
+    assert np.array_equal(outs[0][0], outs[2][0])
+    for a, b in zip(outs[0][1:], outs[2][1:]):
+        assert O.normwise_err(a, b) < TOL
+
+
+def test_basis_only_forward(dev):
+    """y = NULL -> chebyshev2 / lib/graph.py::chebyshev analogue."""
+    from cnn_graph_amd import ops
+    c = case(load_golden("golden_A.npz"))
+    plan = make_plan(c, "auto")
+    basis, y = ops.cheb_forward(plan, t(c["x"], dev), None, c["K"])
+    assert y is None
+    assert np.array_equal(basis.cpu().numpy(), c["basis"])
+
+
+def test_autograd_graphconv_chebyshev5(dev):
+    """The drop-in GraphConv.chebyshev5 through torch autograd."""
+    from cnn_graph_amd.graph_conv import GraphConv
+    g = load_golden("golden_A.npz")
+    c = case(g)
+    L = scipy.sparse.csr_matrix((g["L_data"], g["L_indices"], g["L_indptr"]), shape=tuple(g["L_shape"]))
+    model = GraphConv(filter="chebyshev5", device=dev)
+    with model.variable_scope("conv1"):
+        x = t(c["x"], dev).requires_grad_(True)
+        W = model._weight_variable([c["K"], c["Fout"]], regularization=False)
+        with torch.no_grad():
+            W.copy_(t(c["W"], dev))
+        y = model.filter(x, L, c["Fout"], c["K"])
+    y.backward(t(c["dy"], dev))
+    assert O.normwise_err(y.detach().cpu().numpy(), c["y_ref"]) < TOL
+    assert O.normwise_err(x.grad.cpu().numpy(), c["dx_ref"]) < TOL
+    assert O.normwise_err(W.grad.cpu().numpy(), c["dW_ref"]) < TOL
+    assert list(model.weights) == ["conv1/weights"]
+
+
+def test_maxpool_avgpool_vs_oracle(dev):
+    from cnn_graph_amd import ops
+    x = load_golden("golden_misc.npz")["pool_x"]
+    for p in (2, 4, 8):
+        xt = t(x, dev).requires_grad_(True)
+        y, arg = ops.mpool1_with_argmax(xt, p)
+        oy, oarg = O.mpool1_forward(x, p)
+        assert np.array_equal(y.detach().cpu().numpy(), oy)
+        assert np.array_equal(arg.cpu().numpy(), oarg)
+        dy = np.random.default_rng(p).standard_normal(oy.shape).astype(np.float32)
+        y.backward(t(dy, dev))
+        assert np.array_equal(xt.grad.cpu().numpy(), O.mpool1_backward(dy, oarg, x.shape[1]))
+        xa = t(x, dev).requires_grad_(True)
+        ya = ops.apool1(xa, p)
+        np.testing.assert_allclose(ya.detach().cpu().numpy(), O.apool1_forward(x, p), rtol=1e-6)
+        ya.sum().backward()
+        np.testing.assert_allclose(xa.grad.cpu().numpy(), np.full(x.shape, 1.0 / p, np.float32))
+
+
+def test_perm_data_vs_reference(dev):
+    from cnn_graph_amd import ops
+    g = load_golden("golden_B.npz")
+    out = ops.perm_data(t(g["pdata_in"], dev), g["perm0"])
+    assert np.array_equal(out.cpu().numpy(), g["pdata_out"].astype(np.float32))
+    x3 = np.random.default_rng(1).random((3, 784, 5), dtype=np.float32)
+    out3 = ops.perm_data(t(x3, dev), g["perm0"])
+    assert np.array_equal(out3.cpu().numpy(), O.perm_data(x3, g["perm0"]))
+
+
+def test_adam_vs_oracle(dev):
+    from cnn_graph_amd import ops
+    rng = np.random.default_rng(4)
+    p = rng.standard_normal(800).astype(np.float32)
+    m = np.zeros(800, np.float32)
+    v = np.zeros(800, np.float32)
+    P, Mt, Vt = t(p, dev), t(m, dev), t(v, dev)
+    ref = (p.astype(np.float64), m.astype(np.float64), v.astype(np.float64))
+    for step in range(1, 6):
+        gr = rng.standard_normal(800).astype(np.float32)
+        ops.adam_update(P, t(gr * 2, dev), Mt, Vt, step, lr=0.01, grad_scale=0.5)
+        ref = O.adam_step(*ref[:1], gr.astype(np.float64), ref[1], ref[2], step, lr=0.01)
+    np.testing.assert_allclose(P.cpu().numpy(), ref[0], rtol=1e-5, atol=1e-6)
+
+
+def test_bad_shapes_raise(dev):
+    from cnn_graph_amd import ops, _lib
+    c = case(load_golden("golden_A.npz"))
+    plan = make_plan(c, "auto")
+    with pytest.raises(ValueError):
+        ops.cheb_forward(plan, torch.zeros((2, c["M"] + 1, 1), device=dev), t(c["W"], dev), c["K"])
+    with pytest.raises(ValueError):
+        ops.cheb_forward(plan, torch.zeros((2, c["M"], 1)), None, c["K"])  # CPU tensor: no fallback
+    big = make_plan(c, "resident")
+    with pytest.raises(_lib.CGError):
+        ops.cheb_forward(big, torch.zeros((1, c["M"], 4096), device=dev), None, 40)
