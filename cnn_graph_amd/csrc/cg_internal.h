@@ -8,7 +8,7 @@
 namespace cg {
 
 constexpr int kWave = 64;
-constexpr int kResidentThreads = 512;  // 8 waves: two per SIMD, one workgroup per CU
+constexpr int kResidentThreads = 1024;  // 16 waves: four per SIMD, one workgroup per CU
 constexpr int kLdsBytes = 160 * 1024;  // gfx950 LDS per CU
 
 // Padded LDS row stride for a vertex vector: >= M, == 1 (mod 32) so that the
@@ -17,25 +17,32 @@ constexpr int kLdsBytes = 160 * 1024;  // gfx950 LDS per CU
 __host__ __device__ inline int lds_vertex_stride(int M) { return ((M + 31) / 32) * 32 + 1; }
 __host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
+// Ablation switches for timing experiments only (never set in production):
+// bits 0-7 forward resident kernel, bits 8-15 backward.  See cg_debug_set_flags.
+extern int g_debug_flags;
+
 // ---- resident (LDS) path ---------------------------------------------------
 struct ResidentGeom {
-  int mt;          // m-tiles of 32 vertices per wave (template arg, >= needed)
-  int nt;          // 32-wide tiles over Fout (forward) (template arg)
+  int rpt;         // CSR rows per thread (ceil(M / 1024)), template arg
+  int nt;          // 32-wide tiles over Fout (forward), template arg
+  int maxnnz;      // register slots per row of L~ (forward), template arg
+  int maxnnzT;     // register slots per row of L~^T (backward), template arg
   size_t fwd_lds;  // dynamic LDS bytes of the forward kernel
   size_t bwd_lds;  // dynamic LDS bytes of the backward kernel
+  bool stage;      // forward stages the sample's basis in LDS and stores it coalesced
   bool fwd_ok;
   bool bwd_ok;
 };
-ResidentGeom resident_geometry(int M, int64_t nnz, int64_t nnzT, int Fin, int K, int Fout);
+ResidentGeom resident_geometry(int M, int max_row_nnz, int max_row_nnzT, int Fin, int K, int Fout);
 
 hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                   int nnz, const int* rowptr, const uint16_t* col16,
-                                   const float* val, const float* x, const float* W, float* basis,
-                                   float* y, hipStream_t s);
+                                   const int* rowptr, const int* col, const float* val,
+                                   const float* x, const float* W, float* basis, float* y,
+                                   hipStream_t s);
 hipError_t launch_resident_backward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                    int nnzT, const int* trowptr, const uint16_t* tcol16,
-                                    const float* tval, const float* dy, const float* basis,
-                                    const float* W, float* dx, float* dw_slab, hipStream_t s);
+                                    const int* trowptr, const int* tcol, const float* tval,
+                                    const float* dy, const float* basis, const float* W, float* dx,
+                                    float* dw_slab, hipStream_t s);
 
 // ---- streaming path ----------------------------------------------------------
 hipError_t launch_x_to_cols(const float* x, float* T0, float* basis, int N, int M, int Fin, int K,

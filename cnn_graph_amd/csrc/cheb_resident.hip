@@ -1,48 +1,123 @@
 // Resident (LDS) path of the Chebyshev graph convolution for gfx950.
 //
-// One 512-thread workgroup per sample n.  The whole K-step recurrence
+// One 1024-thread workgroup (16 waves, 4 per SIMD) per sample n.  The whole
+// K-step recurrence
 //   T_0 = X, T_1 = L~X, T_k = 2 L~ T_{k-1} - T_{k-2}      (lib/graph_conv.py:163-169)
-// runs out of LDS: the CSR of L~ (uint16 columns) and a 3-slot ring of
-// vertex vectors stay on chip, so HBM sees only x in, the basis out (layout of
-// lib/graph_conv.py:172) and y out.  The weight contraction
-//   y = basis @ W                                          (lib/graph_conv.py:175)
-// is folded into the recurrence: every two steps each wave feeds the pair
-// (T_{2s}, T_{2s+1}) of its 32-vertex tiles to v_mfma_f32_32x32x2_f32, whose
-// K=2 is exactly one Chebyshev pair, accumulating y in registers.
+// runs on chip: each thread owns RPT rows of L~ and keeps their CSR entries
+// (column, value) in REGISTERS for the whole launch -- the sparse operand is
+// read from L2 once per workgroup -- while a 3-slot ring of vertex vectors
+// lives in LDS.  A step is one burst of independent LDS gathers per row, a
+// sequential fp32 accumulation, and one barrier.
+//
+// The weight contraction y = basis @ W (lib/graph_conv.py:175) is folded into
+// the recurrence: every two steps each wave feeds the pair (T_{2s}, T_{2s+1})
+// of its 32-vertex tiles to v_mfma_f32_32x32x2_f32, whose K=2 is exactly one
+// Chebyshev pair, accumulating y in registers.  The same A-operand values are
+// the basis entries: they are staged in LDS in the HBM layout of
+// lib/graph_conv.py:172 ([m][fin*K+k], a contiguous block per sample) and
+// leave with fully coalesced stores at the end (a row of that layout is only
+// complete after the last step, so streaming it earlier would write partial
+// lines -- measured 28 us of scattered 4-byte stores on config B).
 //
 // The backward kernel does, per sample:
 //   A. dBasis = dy W^T on MFMA into LDS (D[j][m], j = fin*K + k);
-//   B. the reverse (Clenshaw) recurrence over L~^T in LDS
+//   B. the reverse (Clenshaw) recurrence over L~^T (CSR in registers)
 //        G_{K-1} = D_{K-1};  G_k = D_k + 2 L~^T G_{k+1} - G_{k+2};  G_0 = D_0 + L~^T G_1 - G_2
 //      writing dx = G_0 straight to HBM;
 //   C. the per-sample dW partial basis^T dy on MFMA (waves split the vertex
 //      range, summed across waves through LDS in a fixed order -> deterministic),
-//      written to a slab reduced over samples by a second tiny kernel.
+//      written to a slab reduced over samples by k_reduce_slabs.
+// All global loads are issued unconditionally from clamped addresses and
+// masked afterwards, so hipcc does not branch around each load (one vmcnt(0)
+// per element, guide §5 "Three .s-level traps" (c)).
 //
-// Numerics: the SpMM accumulates each row sequentially from 0 in CSR order,
-// one rounding per product and per add (fp contraction OFF) -- the order of
-// scipy csr_matvecs / TF SparseTensorDenseMatMul -- so the basis is bit-exact
-// to lib/graph.py::chebyshev.  MFMA f32 is an exact fp32 fma chain.
+// Numerics: each row accumulates sequentially from 0 in CSR order with one
+// rounding per product and per add (fp contraction OFF) -- the order of scipy
+// csr_matvecs / TF SparseTensorDenseMatMul -- so the basis is bit-exact to
+// lib/graph.py::chebyshev.  MFMA f32 is an exact fp32 fma chain.
 #include "cg_internal.h"
 
 namespace cg {
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kT = kResidentThreads;  // 1024
+constexpr int kWaves = kT / 64;       // 16
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = imax(v, __shfl_xor(v, o));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Register-resident CSR rows of one thread: rows tid, tid + kT, ...
+template <int RPT, int MAXNNZ>
+struct RowRegs {
+  int beg[RPT];
+  int len[RPT];
+  int wmax[RPT];  // wave-uniform max(len) over the wave's rows: gathers beyond it are skipped
+  int c[RPT][MAXNNZ];
+  float v[RPT][MAXNNZ];
+
+  __device__ __forceinline__ void load(int tid, int M, const int* __restrict__ rowptr,
+                                       const int* __restrict__ col,
+                                       const float* __restrict__ val) {
+    const int nnz = rowptr[M];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int r = imin(tid + q * kT, M - 1);
+      const bool own = (tid + q * kT) < M;
+      const int b0 = rowptr[r], b1 = rowptr[r + 1];
+      beg[q] = b0;
+      len[q] = own ? b1 - b0 : 0;
+      wmax[q] = wave_max(len[q]);
+#pragma unroll
+      for (int j = 0; j < MAXNNZ; ++j) {
+        const int idx = imax(imin(b0 + j, nnz - 1), 0);  // clamped: always a valid address
+        const int cj = nnz > 0 ? col[idx] : 0;
+        const float vj = nnz > 0 ? val[idx] : 0.f;
+        const bool in = j < len[q];
+        c[q][j] = in ? cj : 0;  // padding gathers vertex 0 (always in range)
+        v[q][j] = in ? vj : 0.f;
+      }
+    }
+  }
+
+  // sum_{j in row, CSR order} v_j * T[c_j]   (sequential, no contraction)
+  __device__ __forceinline__ float dot(int q, const float* __restrict__ T,
+                                       const int* __restrict__ col,
+                                       const float* __restrict__ val) const {
+#pragma clang fp contract(off)
+    float g[MAXNNZ];
+#pragma unroll
+    for (int j = 0; j < MAXNNZ; ++j) g[j] = (j < wmax[q]) ? T[c[q][j]] : 0.f;  // LDS gathers
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXNNZ; ++j)
+      if (j < len[q]) a = a + v[q][j] * g[j];
+    if (wmax[q] > MAXNNZ)  // rows longer than MAXNNZ (rare): global CSR tail
+      for (int j = MAXNNZ; j < len[q]; ++j) a = a + val[beg[q] + j] * T[col[beg[q] + j]];
+    return a;
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Forward
 // ---------------------------------------------------------------------------
-template <int MT, int NT>
-__global__ __launch_bounds__(kResidentThreads) void cheb_fwd_resident(
-    int M, int Fin, int K, int Fout, int nnz, int Mp, const int* __restrict__ rowptr,
-    const uint16_t* __restrict__ col16, const float* __restrict__ val, const float* __restrict__ x,
+template <int RPT, int MAXNNZ, int NT>
+__global__ __launch_bounds__(kT) void cheb_fwd_resident(
+    int M, int Fin, int K, int Fout, int Mp, int stage, int dbg, const int* __restrict__ rowptr,
+    const int* __restrict__ col, const float* __restrict__ val, const float* __restrict__ x,
     const float* __restrict__ W, float* __restrict__ basis, float* __restrict__ y) {
 #pragma clang fp contract(off)
+  constexpr int MT = 2 * RPT;  // 32-vertex tiles per wave: ceil(M/32)/16 <= 2*RPT
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
@@ -51,28 +126,22 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_fwd_resident(
   const int h = lane >> 5, li = lane & 31;
   const int FinK = Fin * K;
 
-  int* s_rp = reinterpret_cast<int*>(smem);
-  size_t off = align16(size_t(M + 1) * 4);
-  uint16_t* s_col = reinterpret_cast<uint16_t*>(smem + off);
-  off = align16(off + size_t(nnz) * 2);
-  float* s_val = reinterpret_cast<float*>(smem + off);
-  off = align16(off + size_t(nnz) * 4);
-  float* s_W = reinterpret_cast<float*>(smem + off);
-  off = align16(off + size_t(FinK) * Fout * 4);
+  float* s_W = reinterpret_cast<float*>(smem);
+  size_t off = align16(size_t(FinK) * Fout * 4);
   float* s_T = reinterpret_cast<float*>(smem + off);  // [3][Fin][Mp]
+  off = align16(off + size_t(3) * Fin * Mp * 4);
+  float* s_B = reinterpret_cast<float*>(smem + off);  // [M][FinK] (stage only)
 
-  for (int i = tid; i <= M; i += kResidentThreads) s_rp[i] = rowptr[i];
-  for (int i = tid; i < nnz; i += kResidentThreads) {
-    s_col[i] = col16[i];
-    s_val[i] = val[i];
-  }
-  for (int i = tid; i < FinK * Fout; i += kResidentThreads) s_W[i] = W ? W[i] : 0.f;
+  RowRegs<RPT, MAXNNZ> rows;
+  rows.load(tid, M, rowptr, col, val);
+  for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = W ? W[i] : 0.f;
   const float* xn = x + size_t(n) * M * Fin;
-  for (int i = tid; i < M * Fin; i += kResidentThreads) {
+  for (int i = tid; i < M * Fin; i += kT) {
     const int m = i / Fin, fin = i - m * Fin;
     s_T[fin * Mp + m] = xn[i];  // slot 0 = T_0
   }
   __syncthreads();
+  if (dbg & 16) return;
 
   const int ntiles = (M + 31) >> 5;
   f32x16 acc[MT][NT];
@@ -84,9 +153,8 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_fwd_resident(
       for (int r = 0; r < 16; ++r) acc[t][q][r] = 0.f;
 
   float* basis_n = basis ? basis + size_t(n) * M * FinK : nullptr;
+  const bool keep_basis = basis_n && !(dbg & 2);
 
-  // Contraction of the Chebyshev pair (T_{2s}, T_{2s+1}) on MFMA; also stores
-  // those basis entries (both already in registers as the A operand).
   auto mfma_pair = [&](int s) {
     const int kk = 2 * s + h;
     const bool kv = kk < K;
@@ -101,16 +169,24 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_fwd_resident(
       const float* Ts = s_T + (slot * Fin + fin) * Mp;
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
-        const int tile = wave + t * 8;
+        const int tile = wave + t * kWaves;
         if (tile < ntiles) {
           const int m = tile * 32 + li;
           float a = 0.f;
           if (kv && m < M) {
             a = Ts[m];
-            if (basis_n) basis_n[size_t(m) * FinK + fin * K + kk] = a;
+            if (keep_basis) {
+              const int e = m * FinK + fin * K + kk;
+              if (stage)
+                s_B[e] = a;  // banks (25*li + kk) mod 32: conflict-free for odd FinK
+              else
+                basis_n[e] = a;
+            }
           }
+          if (!(dbg & 4)) {
 #pragma unroll
-          for (int q = 0; q < NT; ++q) acc[t][q] = mfma32(a, b[q], acc[t][q]);
+            for (int q = 0; q < NT; ++q) acc[t][q] = mfma32(a, b[q], acc[t][q]);
+          }
         }
       }
     }
@@ -123,22 +199,38 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_fwd_resident(
       const float* Tp = s_T + (prv * Fin + fin) * Mp;
       const float* Tp2 = s_T + (prv2 * Fin + fin) * Mp;
       float* To = s_T + (cur * Fin + fin) * Mp;
-      for (int r = tid; r < M; r += kResidentThreads) {
-        const int j0 = s_rp[r], j1 = s_rp[r + 1];
-        float a = 0.f;
-        for (int j = j0; j < j1; ++j) a = a + s_val[j] * Tp[s_col[j]];
-        To[r] = (k == 1) ? a : (2.f * a - Tp2[r]);
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        const int r = tid + q * kT;
+        if (r < M) {
+          const float a = (dbg & 1) ? Tp[r] : rows.dot(q, Tp, col, val);
+          To[r] = (k == 1) ? a : (2.f * a - Tp2[r]);
+        }
       }
     }
     __syncthreads();
   }
   mfma_pair((K - 1) >> 1);  // the last (possibly half-empty) pair
 
-  if (y) {
+  if (keep_basis && stage) {
+    __syncthreads();
+    const int total = M * FinK;
+    if ((reinterpret_cast<uintptr_t>(basis_n) & 15) == 0) {
+      const int n4 = total >> 2;
+      const float4* src = reinterpret_cast<const float4*>(s_B);
+      float4* dst = reinterpret_cast<float4*>(basis_n);
+      for (int i = tid; i < n4; i += kT) dst[i] = src[i];
+      for (int i = (n4 << 2) + tid; i < total; i += kT) basis_n[i] = s_B[i];
+    } else {
+      for (int i = tid; i < total; i += kT) basis_n[i] = s_B[i];
+    }
+  }
+
+  if (y && !(dbg & 8)) {
     float* yn = y + size_t(n) * M * Fout;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      const int tile = wave + t * 8;
+      const int tile = wave + t * kWaves;
       if (tile < ntiles) {
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
@@ -157,11 +249,12 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_fwd_resident(
 // ---------------------------------------------------------------------------
 // Backward
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kResidentThreads) void cheb_bwd_resident(
-    int M, int Fin, int K, int Fout, int nnzT, int Mp, const int* __restrict__ trowptr,
-    const uint16_t* __restrict__ tcol16, const float* __restrict__ tval,
-    const float* __restrict__ dy, const float* __restrict__ basis, const float* __restrict__ W,
-    float* __restrict__ dx, float* __restrict__ dw_slab) {
+template <int RPT, int MAXNNZ>
+__global__ __launch_bounds__(kT) void cheb_bwd_resident(
+    int M, int Fin, int K, int Fout, int Mp, int dbg, const int* __restrict__ trowptr,
+    const int* __restrict__ tcol, const float* __restrict__ tval, const float* __restrict__ dy,
+    const float* __restrict__ basis, const float* __restrict__ W, float* __restrict__ dx,
+    float* __restrict__ dw_slab) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.x;
@@ -171,46 +264,53 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_bwd_resident(
   const int h = lane >> 5, li = lane & 31;
   const int FinK = Fin * K;
 
-  int* s_rp = reinterpret_cast<int*>(smem);
-  size_t off = align16(size_t(M + 1) * 4);
-  uint16_t* s_col = reinterpret_cast<uint16_t*>(smem + off);
-  off = align16(off + size_t(nnzT) * 2);
-  float* s_val = reinterpret_cast<float*>(smem + off);
-  off = align16(off + size_t(nnzT) * 4);
-  float* s_D = reinterpret_cast<float*>(smem + off);  // [FinK][Mp], later dW scratch
   const size_t dbytes = size_t(FinK) * Mp * 4;
-  off = align16(off + (dbytes > 32768 ? dbytes : 32768));
+  constexpr size_t kScratch = size_t(kWaves) * 32 * 32 * 4;
+  float* s_D = reinterpret_cast<float*>(smem);  // [FinK][Mp], later dW scratch [16][32][32]
+  size_t off = align16(dbytes > kScratch ? dbytes : kScratch);
   float* s_G = reinterpret_cast<float*>(smem + off);  // [3][Fin][Mp]
+  off = align16(off + size_t(3) * Fin * Mp * 4);
+  float* s_W = reinterpret_cast<float*>(smem + off);  // [FinK][Fout]
 
-  for (int i = tid; i <= M; i += kResidentThreads) s_rp[i] = trowptr[i];
-  for (int i = tid; i < nnzT; i += kResidentThreads) {
-    s_col[i] = tcol16[i];
-    s_val[i] = tval[i];
-  }
+  RowRegs<RPT, MAXNNZ> rows;
+  rows.load(tid, M, trowptr, tcol, tval);
+  for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = W[i];
+  __syncthreads();
+  if (dbg & 16) return;
 
   const float* dyn = dy + size_t(n) * M * Fout;
   const float* bn = basis + size_t(n) * M * FinK;
 
   // A. dBasis = dy W^T  (rows m, cols j, inner f; lane half h owns f in [h*ns, h*ns+ns))
-  {
+  if (!(dbg & 1)) {
     const int mtiles = (M + 31) >> 5, jtiles = (FinK + 31) >> 5;
     const int ns = (Fout + 1) >> 1;
-    for (int task = wave; task < mtiles * jtiles; task += 8) {
+    for (int task = wave; task < mtiles * jtiles; task += kWaves) {
       const int mt = task / jtiles, jt = task - mt * jtiles;
       const int m = mt * 32 + li, j = jt * 32 + li;
-      const float* dyrow = dyn + size_t(m) * Fout;
-      const float* wrow = W + size_t(j) * Fout;
+      const bool mv = m < M, jv = j < FinK;
+      const float* dyrow = dyn + size_t(imin(m, M - 1)) * Fout;
+      const float* wrow = s_W + imin(j, FinK - 1) * Fout;
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll 4
-      for (int s = 0; s < ns; ++s) {
-        const int f = h * ns + s;
-        const float a = (m < M && f < Fout) ? dyrow[f] : 0.f;
-        const float b = (j < FinK && f < Fout) ? wrow[f] : 0.f;
-        acc = mfma32(a, b, acc);
+      for (int s0 = 0; s0 < ns; s0 += 8) {
+        float a[8], b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {  // 8 independent loads in flight
+          const int f = h * ns + s0 + u;
+          const int fc = imin(f, Fout - 1);
+          a[u] = dyrow[fc];
+          b[u] = wrow[fc];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int f = h * ns + s0 + u;
+          const bool fv = (s0 + u) < ns && f < Fout;
+          acc = mfma32((mv && fv) ? a[u] : 0.f, (jv && fv) ? b[u] : 0.f, acc);
+        }
       }
-      if (j < FinK) {
+      if (jv) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -231,43 +331,52 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_bwd_resident(
       const float* G2 = s_G + (nx2 * Fin + fin) * Mp;
       float* Go = s_G + (cur * Fin + fin) * Mp;
       const float* Dk = s_D + (fin * K + k) * Mp;
-      for (int r = tid; r < M; r += kResidentThreads) {
-        float a = 0.f;
-        if (has1) {
-          const int j0 = s_rp[r], j1 = s_rp[r + 1];
-          for (int j = j0; j < j1; ++j) a = a + s_val[j] * G1[s_col[j]];
-        }
-        float g = Dk[r] + c * a;
-        if (has2) g = g - G2[r];
-        if (k == 0) {
-          if (dx) dx[(size_t(n) * M + r) * Fin + fin] = g;
-        } else {
-          Go[r] = g;
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) {
+        const int r = tid + q * kT;
+        if (r < M) {
+          const float a = has1 ? ((dbg & 2) ? G1[r] : rows.dot(q, G1, tcol, tval)) : 0.f;
+          float g = Dk[r] + c * a;
+          if (has2) g = g - G2[r];
+          if (k == 0) {
+            if (dx) dx[(size_t(n) * M + r) * Fin + fin] = g;
+          } else {
+            Go[r] = g;
+          }
         }
       }
     }
     if (k > 0) __syncthreads();
   }
 
-  // C. dW partial = basis^T dy (rows j, cols f, inner m split over the 8 waves)
-  {
+  // C. dW partial = basis^T dy (rows j, cols f, inner m split over the 16 waves)
+  if (!(dbg & 4)) {
     const int jtl = (FinK + 31) >> 5, ftl = (Fout + 31) >> 5;
-    const int chunk = (((M + 7) >> 3) + 1) & ~1;
+    const int chunk = (((M + kWaves - 1) / kWaves) + 1) & ~1;
     const int mbeg = wave * chunk;
-    const int mend = (mbeg + chunk < M) ? (mbeg + chunk) : M;
-    float* scratch = s_D;  // [8][32][32]
+    const int mend = imin(mbeg + chunk, M);
+    float* scratch = s_D;  // [16][32][32]
     for (int task = 0; task < jtl * ftl; ++task) {
       const int jt = task / ftl, ft = task - jt * ftl;
       const int j = jt * 32 + li, f = ft * 32 + li;
+      const bool jv = j < FinK, fv = f < Fout;
+      const int jc = imin(j, FinK - 1), fc = imin(f, Fout - 1);
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll 8
-      for (int mm = mbeg; mm < mend; mm += 2) {
-        const int m = mm + h;
-        const float a = (m < mend && j < FinK) ? bn[size_t(m) * FinK + j] : 0.f;
-        const float b = (m < mend && f < Fout) ? dyn[size_t(m) * Fout + f] : 0.f;
-        acc = mfma32(a, b, acc);
+      for (int mm0 = mbeg; mm0 < mend; mm0 += 16) {
+        float a[8], b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {  // 16 independent loads in flight
+          const int mc = imin(mm0 + 2 * u + h, M - 1);
+          a[u] = bn[size_t(mc) * FinK + jc];
+          b[u] = dyn[size_t(mc) * Fout + fc];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool mv = (mm0 + 2 * u + h) < mend;
+          acc = mfma32((mv && jv) ? a[u] : 0.f, (mv && fv) ? b[u] : 0.f, acc);
+        }
       }
       __syncthreads();  // s_D free (phase B done) / previous task's readers done
 #pragma unroll
@@ -276,86 +385,106 @@ __global__ __launch_bounds__(kResidentThreads) void cheb_bwd_resident(
         scratch[(wave * 32 + row) * 32 + li] = acc[r];
       }
       __syncthreads();
-      for (int e = tid; e < 1024; e += kResidentThreads) {
-        const int row = e >> 5, col = e & 31;
+      for (int e = tid; e < 1024; e += kT) {
+        const int row = e >> 5, cc = e & 31;
         float s = 0.f;
 #pragma unroll
-        for (int w = 0; w < 8; ++w) s = s + scratch[(w * 32 + row) * 32 + col];
-        const int jj = jt * 32 + row, ff = ft * 32 + col;
+        for (int w = 0; w < kWaves; ++w) s = s + scratch[(w * 32 + row) * 32 + cc];
+        const int jj = jt * 32 + row, ff = ft * 32 + cc;
         if (jj < FinK && ff < Fout) dw_slab[(size_t(n) * FinK + jj) * Fout + ff] = s;
       }
     }
   }
 }
 
-template <int MT, int NT>
-hipError_t launch_fwd_t(size_t lds, int N, int M, int Fin, int K, int Fout, int nnz,
-                        const int* rowptr, const uint16_t* col16, const float* val,
-                        const float* x, const float* W, float* basis, float* y, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cheb_fwd_resident<MT, NT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((cheb_fwd_resident<MT, NT>), dim3(N), dim3(kResidentThreads), lds, s, M, Fin,
-                     K, Fout, nnz, lds_vertex_stride(M), rowptr, col16, val, x, W, basis, y);
+template <typename Kern>
+hipError_t allow_big_lds(Kern k) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+}
+
+template <int RPT, int MAXNNZ, int NT>
+hipError_t launch_fwd_t(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
+                        const int* rowptr, const int* col, const float* val, const float* x,
+                        const float* W, float* basis, float* y, hipStream_t s) {
+  static hipError_t attr = allow_big_lds(&cheb_fwd_resident<RPT, MAXNNZ, NT>);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((cheb_fwd_resident<RPT, MAXNNZ, NT>), dim3(N), dim3(kT), g.fwd_lds, s, M, Fin,
+                     K, Fout, lds_vertex_stride(M), int(g.stage), g_debug_flags & 0xff, rowptr,
+                     col, val, x, W, basis, y);
   return hipGetLastError();
+}
+
+template <int RPT, int MAXNNZ>
+hipError_t launch_bwd_t(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
+                        const int* trowptr, const int* tcol, const float* tval, const float* dy,
+                        const float* basis, const float* W, float* dx, float* dw_slab,
+                        hipStream_t s) {
+  static hipError_t attr = allow_big_lds(&cheb_bwd_resident<RPT, MAXNNZ>);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((cheb_bwd_resident<RPT, MAXNNZ>), dim3(N), dim3(kT), g.bwd_lds, s, M, Fin, K,
+                     Fout, lds_vertex_stride(M), (g_debug_flags >> 8) & 0xff, trowptr, tcol, tval,
+                     dy, basis, W, dx, dw_slab);
+  return hipGetLastError();
+}
+
+int pick_maxnnz(int rpt, int max_row_nnz) {
+  if (max_row_nnz <= 12) return 12;
+  if (max_row_nnz <= 16) return 16;
+  return rpt == 1 ? 32 : 16;  // longer rows take the (rare) global-CSR tail loop
 }
 
 }  // namespace
 
-ResidentGeom resident_geometry(int M, int64_t nnz, int64_t nnzT, int Fin, int K, int Fout) {
+ResidentGeom resident_geometry(int M, int max_row_nnz, int max_row_nnzT, int Fin, int K,
+                               int Fout) {
   ResidentGeom g{};
   const int Mp = lds_vertex_stride(M);
-  const int ntiles = (M + 31) / 32;
-  const int need_mt = (ntiles + 7) / 8;
-  int mt = 1;
-  while (mt < need_mt) mt <<= 1;
-  const int nt = (Fout + 31) / 32;
-  g.mt = mt;
-  g.nt = nt;
+  g.rpt = (M + kT - 1) / kT;
+  g.nt = (Fout + 31) / 32;
+  g.maxnnz = pick_maxnnz(g.rpt, max_row_nnz);
+  g.maxnnzT = pick_maxnnz(g.rpt, max_row_nnzT);
   const size_t FinK = size_t(Fin) * K;
-  g.fwd_lds = align16(size_t(M + 1) * 4) + align16(size_t(nnz) * 2) + align16(size_t(nnz) * 4) +
-              align16(FinK * Fout * 4) + size_t(3) * Fin * Mp * 4;
+  const size_t base = align16(FinK * Fout * 4) + align16(size_t(3) * Fin * Mp * 4);
+  const size_t staged = base + size_t(M) * FinK * 4;
+  g.stage = staged <= size_t(kLdsBytes);
+  g.fwd_lds = g.stage ? staged : base;
   const size_t dbytes = FinK * Mp * 4;
-  g.bwd_lds = align16(size_t(M + 1) * 4) + align16(size_t(nnzT) * 2) + align16(size_t(nnzT) * 4) +
-              align16(dbytes > 32768 ? dbytes : 32768) + size_t(3) * Fin * Mp * 4;
-  const bool small = M >= 1 && M <= 65535 && Fin >= 1 && K >= 1 && Fout >= 1;
-  g.fwd_ok = small && need_mt <= 8 && nt <= 2 && mt * nt <= 8 && g.fwd_lds <= size_t(kLdsBytes);
-  g.bwd_ok = small && g.bwd_lds <= size_t(kLdsBytes);
+  const size_t scratch = size_t(kWaves) * 32 * 32 * 4;
+  g.bwd_lds = align16(dbytes > scratch ? dbytes : scratch) + align16(size_t(3) * Fin * Mp * 4) +
+              FinK * Fout * 4;
+  const bool shape_ok = M >= 1 && Fin >= 1 && K >= 1 && Fout >= 1 && g.rpt <= 2;
+  // RPT=2 with two Fout tiles spills hundreds of VGPRs: leave it to the streaming path
+  g.fwd_ok = shape_ok && g.nt <= 2 && !(g.rpt == 2 && g.nt == 2) && g.fwd_lds <= size_t(kLdsBytes);
+  g.bwd_ok = shape_ok && g.bwd_lds <= size_t(kLdsBytes);
   return g;
 }
 
 hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                   int nnz, const int* rowptr, const uint16_t* col16,
-                                   const float* val, const float* x, const float* W, float* basis,
-                                   float* y, hipStream_t s) {
-#define CG_FWD(MT_, NT_)                                                                       \
-  if (g.mt == MT_ && g.nt == NT_)                                                              \
-    return launch_fwd_t<MT_, NT_>(g.fwd_lds, N, M, Fin, K, Fout, nnz, rowptr, col16, val, x, W, \
-                                  basis, y, s);
-  CG_FWD(1, 1) CG_FWD(2, 1) CG_FWD(4, 1) CG_FWD(8, 1) CG_FWD(1, 2) CG_FWD(2, 2) CG_FWD(4, 2)
+                                   const int* rowptr, const int* col, const float* val,
+                                   const float* x, const float* W, float* basis, float* y,
+                                   hipStream_t s) {
+#define CG_FWD(R_, Z_, NT_)                                                                  \
+  if (g.rpt == R_ && g.maxnnz == Z_ && g.nt == NT_)                                          \
+    return launch_fwd_t<R_, Z_, NT_>(g, N, M, Fin, K, Fout, rowptr, col, val, x, W, basis, y, \
+                                     s);
+  CG_FWD(1, 12, 1) CG_FWD(1, 16, 1) CG_FWD(1, 32, 1) CG_FWD(2, 12, 1) CG_FWD(2, 16, 1)
+  CG_FWD(1, 12, 2) CG_FWD(1, 16, 2) CG_FWD(1, 32, 2)
 #undef CG_FWD
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_resident_backward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                    int nnzT, const int* trowptr, const uint16_t* tcol16,
-                                    const float* tval, const float* dy, const float* basis,
-                                    const float* W, float* dx, float* dw_slab, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cheb_bwd_resident),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(cheb_bwd_resident, dim3(N), dim3(kResidentThreads), g.bwd_lds, s, M, Fin, K,
-                     Fout, nnzT, lds_vertex_stride(M), trowptr, tcol16, tval, dy, basis, W, dx,
-                     dw_slab);
-  return hipGetLastError();
+                                    const int* trowptr, const int* tcol, const float* tval,
+                                    const float* dy, const float* basis, const float* W, float* dx,
+                                    float* dw_slab, hipStream_t s) {
+#define CG_BWD(R_, Z_)                                                                  \
+  if (g.rpt == R_ && g.maxnnzT == Z_)                                                   \
+    return launch_bwd_t<R_, Z_>(g, N, M, Fin, K, Fout, trowptr, tcol, tval, dy, basis, W, \
+                                dx, dw_slab, s);
+  CG_BWD(1, 12) CG_BWD(1, 16) CG_BWD(1, 32) CG_BWD(2, 12) CG_BWD(2, 16)
+#undef CG_BWD
+  return hipErrorInvalidValue;
 }
 
 }  // namespace cg

@@ -187,14 +187,28 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int Mg, int Ng, int Kg, const 
   }
 }
 
-__global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ slab, int nslab,
-                                                      int64_t count, float* __restrict__ out) {
+// out[i] = sum_z slab[z][i] in a FIXED order (bitwise reproducible): wave w of
+// a block sums the slabs z = w, w+16, ... for 64 consecutive outputs (one
+// 256-B coalesced load per slab, 8 in flight), then the 16 partial sums are
+// added in wave order through LDS.
+__global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__ slab, int nslab,
+                                                       int64_t count, float* __restrict__ out) {
 #pragma clang fp contract(off)
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
-       i += int64_t(gridDim.x) * blockDim.x) {
-    float s = 0.f;
-    for (int z = 0; z < nslab; ++z) s = s + slab[int64_t(z) * count + i];
-    out[i] = s;
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = int64_t(blockIdx.x) * 64 + lane;
+  float s = 0.f;
+  if (i < count) {
+#pragma unroll 8
+    for (int z = w; z < nslab; z += 16) s = s + slab[int64_t(z) * count + i];
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i < count) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t = t + part[q][lane];
+    out[i] = t;
   }
 }
 
@@ -267,8 +281,8 @@ hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, c
 
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,
                                hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_slabs, dim3(grid_for(count, 256)), dim3(256), 0, s, slab, nslab,
-                     count, out);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(unsigned((count + 63) / 64)), dim3(1024), 0, s, slab,
+                     nslab, count, out);
   return hipGetLastError();
 }
 

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Timing ablations of the resident kernels (outputs are garbage when a flag is
+set -- timing only).  Interleaved rounds in one process (guide §5.4 rule 24).
+
+  python scripts/ablate.py [--batch 256] [--reps 50] [--rounds 5]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from cnn_graph_amd import _lib, ops  # noqa: E402
+from cnn_graph_amd.plan import ChebPlan  # noqa: E402
+
+FWD = {"full": 0, "no_spmm": 1, "no_basis_store": 2, "no_mfma": 4, "no_y_store": 8,
+       "no_stores": 2 | 8, "only_spmm": 2 | 4 | 8, "nothing": 1 | 2 | 4 | 8, "prologue": 16}
+BWD = {"full": 0, "no_phaseA": 1, "no_clenshaw_spmm": 2, "no_phaseC": 4, "only_phaseC": 1 | 2,
+       "only_A": 2 | 4, "only_B": 1 | 4, "no_reduce": 1 << 15, "prologue": 16 | (1 << 15),
+       "nothing": 1 | 2 | 4 | (1 << 15)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--path", default="resident")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    L, fake = bench.load_config_b()
+    K, Fin, Fout, N = 25, 1, 32, args.batch
+    plan = ChebPlan.from_laplacian(L, 2, 0, path=args.path)
+    M = plan.M
+    x = torch.rand((N, M, Fin), device=dev)
+    W = torch.randn((K, Fout), device=dev) * 0.1
+    dy = torch.randn((N, M, Fout), device=dev)
+    r = ops.ChebRunner(plan, N, Fin, K, Fout, dev)
+    h = _lib.lib()
+    h.cg_debug_set_flags.argtypes = [ctypes_int()]
+
+    def t_fwd():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            r.forward(x, W)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.reps * 1e3
+
+    def t_bwd():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            r.backward(dy, W)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.reps * 1e3
+
+    res = {f"fwd:{k}": [] for k in FWD}
+    res.update({f"bwd:{k}": [] for k in BWD})
+    r.forward(x, W)
+    for _ in range(args.rounds):
+        for k, f in FWD.items():
+            h.cg_debug_set_flags(f)
+            res[f"fwd:{k}"].append(t_fwd())
+        for k, f in BWD.items():
+            h.cg_debug_set_flags(f << 8)
+            res[f"bwd:{k}"].append(t_bwd())
+    h.cg_debug_set_flags(0)
+    out = {k: round(float(np.median(v)), 2) for k, v in res.items()}
+    # K sweep: per-step cost = slope of time vs K
+    sweep = {}
+    for Kx in (2, 7, 13, 25):
+        Wx = torch.randn((Kx, Fout), device=dev) * 0.1
+        rx = ops.ChebRunner(plan, N, Fin, Kx, Fout, dev)
+        for name, f in (("fwd_full", 0), ("fwd_nothing", FWD["nothing"]), ("bwd_full", 0),
+                        ("bwd_nothing", BWD["nothing"])):
+            vals = []
+            for _ in range(args.rounds):
+                if name.startswith("fwd"):
+                    h.cg_debug_set_flags(f)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(args.reps):
+                        rx.forward(x, Wx)
+                    e1.record()
+                else:
+                    h.cg_debug_set_flags(f << 8)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(args.reps):
+                        rx.backward(dy, Wx)
+                    e1.record()
+                torch.cuda.synchronize()
+                vals.append(e0.elapsed_time(e1) / args.reps * 1e3)
+            sweep[f"K{Kx}:{name}"] = round(float(np.median(vals)), 2)
+    h.cg_debug_set_flags(0)
+    print(json.dumps({"batch": N, "path": args.path, "us_median": out, "k_sweep": sweep}, indent=1))
+
+
+def ctypes_int():
+    import ctypes
+    return ctypes.c_int
+
+
+if __name__ == "__main__":
+    main()
