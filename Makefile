@@ -1,10 +1,10 @@
 # Builds libcheb_mi355.so (gfx950) in-tree and the oracle's reference build.
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
-CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=$(ARCH)
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=$(ARCH) $(EXTRA)
 SRC_DIR  := cnn_graph_amd/csrc
-OBJ_DIR  := build/obj
-LIB      := cnn_graph_amd/libcheb_mi355.so
+OBJ_DIR  ?= build/obj
+LIB      ?= cnn_graph_amd/libcheb_mi355.so
 SRCS     := $(SRC_DIR)/cheb_resident.hip $(SRC_DIR)/cheb_stream.hip $(SRC_DIR)/graph_ops.hip \
             $(SRC_DIR)/cheb_abi.cpp $(SRC_DIR)/comm.cpp
 OBJS     := $(patsubst $(SRC_DIR)/%,$(OBJ_DIR)/%.o,$(SRCS))

@@ -10,7 +10,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcheb_mi355.so")
+# CG_LIB_PATH: load an alternative in-tree build (kernel-variant experiments)
+LIB_PATH = os.environ.get("CG_LIB_PATH") or os.path.join(_HERE, "libcheb_mi355.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cheb_mi355.h")
 
 CG_OK, CG_ERR_ARG, CG_ERR_HIP, CG_ERR_UNSUPPORTED, CG_ERR_ALLOC, CG_ERR_COMM = range(6)

@@ -8,7 +8,10 @@
 namespace cg {
 
 constexpr int kWave = 64;
-constexpr int kResidentThreads = 1024;  // 16 waves: four per SIMD, one workgroup per CU
+#ifndef CG_RESIDENT_THREADS
+#define CG_RESIDENT_THREADS 1024
+#endif
+constexpr int kResidentThreads = CG_RESIDENT_THREADS;  // 1024: 16 waves, four per SIMD
 constexpr int kLdsBytes = 160 * 1024;  // gfx950 LDS per CU
 
 // Padded LDS row stride for a vertex vector: >= M, == 1 (mod 32) so that the
@@ -23,7 +26,8 @@ extern int g_debug_flags;
 
 // ---- resident (LDS) path ---------------------------------------------------
 struct ResidentGeom {
-  int rpt;         // CSR rows per thread (ceil(M / 1024)), template arg
+  int nnz;         // nonzeros of L~ (== of L~^T); the resident path needs nnz >= 1
+  int rpt;        // CSR rows per thread (ceil(M / 1024)), template arg
   int nt;          // 32-wide tiles over Fout (forward), template arg
   int maxnnz;      // register slots per row of L~ (forward), template arg
   int maxnnzT;     // register slots per row of L~^T (backward), template arg
@@ -33,7 +37,8 @@ struct ResidentGeom {
   bool fwd_ok;
   bool bwd_ok;
 };
-ResidentGeom resident_geometry(int M, int max_row_nnz, int max_row_nnzT, int Fin, int K, int Fout);
+ResidentGeom resident_geometry(int M, int nnz, int max_row_nnz, int max_row_nnzT, int Fin, int K,
+                               int Fout);
 
 hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
                                    const int* rowptr, const int* col, const float* val,
@@ -41,8 +46,7 @@ hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin,
                                    hipStream_t s);
 hipError_t launch_resident_backward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
                                     const int* trowptr, const int* tcol, const float* tval,
-                                    const float* dy, const float* basis, const float* W, float* dx,
-                                    float* dw_slab, hipStream_t s);
+                                    const float* dy, const float* W, float* dx, hipStream_t s);
 
 // ---- streaming path ----------------------------------------------------------
 hipError_t launch_x_to_cols(const float* x, float* T0, float* basis, int N, int M, int Fin, int K,
@@ -60,6 +64,11 @@ hipError_t launch_clenshaw_step(const int* trowptr, const int* tcol, const float
 hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, const float* A,
                            int lda, const float* B, int ldb, float* C, int ldc, int splits,
                            hipStream_t s);
+// dW = basis^T dy as per-chunk partial slabs ([dw_chunks(R)][FinK][Fout]),
+// R = N*M basis rows; reduce with launch_reduce_slabs.
+int dw_chunks(int64_t R);
+hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
+                           float* slab, hipStream_t s);
 // Number of K slices launch_gemm_f32 actually uses for `splits` requested.
 int gemm_effective_splits(int Kg, int splits);
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,

@@ -31,6 +31,8 @@ struct cg_plan {
   int* trowptr = nullptr;
   int* tcol = nullptr;
   float* tval = nullptr;
+  hipStream_t side = nullptr;  // dW kernel runs here, overlapped with the dx recurrence
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace {
@@ -111,6 +113,9 @@ void free_plan(cg_plan* p) {
   void* ptrs[] = {p->rowptr, p->col, p->val, p->trowptr, p->tcol, p->tval};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
+  if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+  if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+  if (p->side) (void)hipStreamDestroy(p->side);
   delete p;
 }
 
@@ -134,7 +139,7 @@ int check_shape(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fou
 
 int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool backward,
                 int* path) {
-  const cg::ResidentGeom g = cg::resident_geometry(p->M, p->max_row_nnz, p->max_row_nnzT, Fin, K, Fout);
+  const cg::ResidentGeom g = cg::resident_geometry(p->M, int(p->nnz), p->max_row_nnz, p->max_row_nnzT, Fin, K, Fout);
   const bool fits = backward ? g.bwd_ok : g.fwd_ok;
   if (p->path == CG_PATH_STREAM) {
     *path = CG_PATH_STREAM;
@@ -153,18 +158,9 @@ int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool bac
 
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
-int dw_splits(int64_t NM, int FinK, int Fout) {
-  const int64_t tiles = int64_t((FinK + 63) / 64) * ((Fout + 63) / 64);
-  int64_t s = std::max<int64_t>(1, 1024 / std::max<int64_t>(tiles, 1));
-  s = std::min<int64_t>(s, std::max<int64_t>(1, NM / 256));
-  return int(s);
-}
-
 struct StreamWs {
-  size_t ring;   // 3 * M * B floats
-  size_t dA;     // N*M*FinK floats
-  size_t slabs;  // S * FinK * Fout floats
-  int S;
+  size_t ring;  // 3 * M * B floats
+  size_t dA;    // N*M*FinK floats
 };
 
 StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout) {
@@ -174,20 +170,35 @@ StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t 
   const int64_t NM = int64_t(N) * p->M;
   w.ring = al256(size_t(3) * size_t(p->M) * size_t(B) * 4);
   w.dA = al256(size_t(NM) * size_t(FinK) * 4);
-  w.S = cg::gemm_effective_splits(int(NM), dw_splits(NM, int(FinK), Fout));
-  w.slabs = al256(size_t(w.S) * size_t(FinK) * size_t(Fout) * 4);
+  (void)Fout;
   return w;
 }
 
+size_t dw_slab_bytes(int64_t R, int FinK, int Fout) {
+  return al256(size_t(cg::dw_chunks(R)) * size_t(FinK) * size_t(Fout) * 4);
+}
+
+// Workspace layout.  forward: [T ring] (streaming path only).
+// backward: [dW slabs][T ring][dBasis] (the last two for the streaming path).
 int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                     size_t* fwd, size_t* bwd) {
   int pf = 0, pb = 0, rc;
   if ((rc = choose_path(p, Fin, K, Fout, false, &pf))) return rc;
   if ((rc = choose_path(p, Fin, K, Fout, true, &pb))) return rc;
   const StreamWs w = stream_ws(p, N, Fin, K, Fout);
+  const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, Fin * K, Fout);
   *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.ring;
-  *bwd = (pb == CG_PATH_RESIDENT) ? al256(size_t(N) * size_t(Fin) * K * Fout * 4)
-                                  : (w.ring + w.dA + w.slabs);
+  *bwd = slabs + ((pb == CG_PATH_RESIDENT) ? 0 : (w.ring + w.dA));
+  return CG_OK;
+}
+
+// Side stream + fork/join events for the dW kernel (created on first use,
+// on the plan's device; never inside graph capture after the first call).
+int ensure_side_stream(cg_plan* p) {
+  if (p->side) return CG_OK;
+  CG_HIP(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+  CG_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+  CG_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
   return CG_OK;
 }
 
@@ -310,7 +321,7 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
   const int M = plan->M;
 
   if (path == CG_PATH_RESIDENT) {
-    const cg::ResidentGeom g = cg::resident_geometry(M, plan->max_row_nnz, plan->max_row_nnzT, Fin, K, Fout);
+    const cg::ResidentGeom g = cg::resident_geometry(M, int(plan->nnz), plan->max_row_nnz, plan->max_row_nnzT, Fin, K, Fout);
     CG_HIP(cg::launch_resident_forward(g, N, M, Fin, K, Fout, plan->rowptr, plan->col, plan->val,
                                        x, y ? W : nullptr, basis, y, s));
     return ok();
@@ -350,34 +361,53 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int M = plan->M;
   const int FinK = Fin * K;
+  const int64_t R = int64_t(N) * M;
+  const int chunks = cg::dw_chunks(R);
 
-  if (path == CG_PATH_RESIDENT) {
-    const cg::ResidentGeom g = cg::resident_geometry(M, plan->max_row_nnz, plan->max_row_nnzT, Fin, K, Fout);
-    float* slab = static_cast<float*>(workspace);
-    CG_HIP(cg::launch_resident_backward(g, N, M, Fin, K, Fout, plan->trowptr, plan->tcol,
-                                        plan->tval, dy, basis, W, dx, slab, s));
-    if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
-      CG_HIP(cg::launch_reduce_slabs(slab, N, int64_t(FinK) * Fout, dW, s));
-    return ok();
-  }
-  const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
+  // dW = basis^T dy is HBM-streaming and independent of the (latency-bound)
+  // dx recurrence: fork it onto the plan's side stream so the two overlap on
+  // the same CUs, join before the fixed-order slab reduction.
+  if ((rc = ensure_side_stream(plan))) return rc;
   char* base = static_cast<char*>(workspace);
-  float* ring = reinterpret_cast<float*>(base);
-  float* dA = reinterpret_cast<float*>(base + w.ring);
-  float* slabs = reinterpret_cast<float*>(base + w.ring + w.dA);
-  const int NM = N * M;
-  // dW = basis^T dy  (split over N*M, fixed-order slab reduction -> deterministic)
-  CG_HIP(cg::launch_gemm_f32(true, false, FinK, Fout, NM, basis, FinK, dy, Fout, slabs, Fout,
-                             dw_splits(NM, FinK, Fout), s));
-  CG_HIP(cg::launch_reduce_slabs(slabs, w.S, int64_t(FinK) * Fout, dW, s));
-  if (!dx) return ok();
-  // dBasis = dy W^T
-  CG_HIP(cg::launch_gemm_f32(false, true, NM, FinK, Fout, dy, Fout, W, Fout, dA, FinK, 1, s));
-  const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
-  auto G = [&](int k) { return ring + size_t(k % 3) * slot; };
-  for (int k = K - 1; k >= 0; --k)
-    CG_HIP(cg::launch_clenshaw_step(plan->trowptr, plan->tcol, plan->tval, G(k + 1), G(k + 2),
-                                    G(k), dA, dx, N, M, Fin, K, k, s));
+  float* slabs = reinterpret_cast<float*>(base);
+  char* rest = base + dw_slab_bytes(R, FinK, Fout);
+  // Measured on MI355X: a hipEventRecord/hipStreamWaitEvent fork+join costs
+  // ~20 us per call, far more than the overlap gains, so it is opt-in
+  // (cg_debug_set_flags bit 21) and dW normally runs on the caller's stream.
+  const bool overlap = dx != nullptr && (cg::g_debug_flags & (1 << 21));
+  hipStream_t sdw = overlap ? plan->side : s;
+  if (overlap) {
+    CG_HIP(hipEventRecord(plan->ev_fork, s));
+    CG_HIP(hipStreamWaitEvent(plan->side, plan->ev_fork, 0));
+  }
+  if (dx) {
+    if (path == CG_PATH_RESIDENT) {
+      const cg::ResidentGeom g = cg::resident_geometry(M, int(plan->nnz), plan->max_row_nnz,
+                                                       plan->max_row_nnzT, Fin, K, Fout);
+      CG_HIP(cg::launch_resident_backward(g, N, M, Fin, K, Fout, plan->trowptr, plan->tcol,
+                                          plan->tval, dy, W, dx, s));
+    } else {
+      const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
+      float* ring = reinterpret_cast<float*>(rest);
+      float* dA = reinterpret_cast<float*>(rest + w.ring);
+      const int NM = N * M;
+      // dBasis = dy W^T, then the reverse recurrence one launch per step
+      CG_HIP(cg::launch_gemm_f32(false, true, NM, FinK, Fout, dy, Fout, W, Fout, dA, FinK, 1, s));
+      const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
+      auto G = [&](int k) { return ring + size_t(k % 3) * slot; };
+      for (int k = K - 1; k >= 0; --k)
+        CG_HIP(cg::launch_clenshaw_step(plan->trowptr, plan->tcol, plan->tval, G(k + 1), G(k + 2),
+                                        G(k), dA, dx, N, M, Fin, K, k, s));
+    }
+  }
+  if (!(cg::g_debug_flags & (1 << 22)))  // ablation hook: skip dW
+    CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, sdw));
+  if (overlap) {
+    CG_HIP(hipEventRecord(plan->ev_join, plan->side));
+    CG_HIP(hipStreamWaitEvent(s, plan->ev_join, 0));
+  }
+  if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
+    CG_HIP(cg::launch_reduce_slabs(slabs, chunks, int64_t(FinK) * Fout, dW, s));
   return ok();
 }
 

@@ -23,10 +23,9 @@
 //   A. dBasis = dy W^T on MFMA into LDS (D[j][m], j = fin*K + k);
 //   B. the reverse (Clenshaw) recurrence over L~^T (CSR in registers)
 //        G_{K-1} = D_{K-1};  G_k = D_k + 2 L~^T G_{k+1} - G_{k+2};  G_0 = D_0 + L~^T G_1 - G_2
-//      writing dx = G_0 straight to HBM;
-//   C. the per-sample dW partial basis^T dy on MFMA (waves split the vertex
-//      range, summed across waves through LDS in a fixed order -> deterministic),
-//      written to a slab reduced over samples by k_reduce_slabs.
+//      writing dx = G_0 straight to HBM.
+// dW = basis^T dy is not computed here: it is HBM-streaming work that the C
+// ABI launches (k_dw_slabs) on a side stream to overlap this latency-bound kernel.
 // All global loads are issued unconditionally from clamped addresses and
 // masked afterwards, so hipcc does not branch around each load (one vmcnt(0)
 // per element, guide §5 "Three .s-level traps" (c)).
@@ -58,18 +57,21 @@ __device__ __forceinline__ int wave_max(int v) {
 }
 
 // Register-resident CSR rows of one thread: rows tid, tid + kT, ...
+// Padding slots (j >= row length) gather vertex index M of the LDS vector,
+// a word that is kept at 0 (the stride Mp > M), with value 0: they add an
+// exact +0 to the running sum (which starts at +0 and so is never -0), so
+// the accumulation needs no per-lane predicate and stays bit-exact.
 template <int RPT, int MAXNNZ>
 struct RowRegs {
   int beg[RPT];
   int len[RPT];
-  int wmax[RPT];  // wave-uniform max(len) over the wave's rows: gathers beyond it are skipped
+  int wmax[RPT];  // wave-uniform max(len) over the wave's rows (tail loop trigger)
   int c[RPT][MAXNNZ];
   float v[RPT][MAXNNZ];
 
-  __device__ __forceinline__ void load(int tid, int M, const int* __restrict__ rowptr,
+  __device__ __forceinline__ void load(int tid, int M, int nnz, const int* __restrict__ rowptr,
                                        const int* __restrict__ col,
                                        const float* __restrict__ val) {
-    const int nnz = rowptr[M];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int r = imin(tid + q * kT, M - 1);
@@ -78,13 +80,14 @@ struct RowRegs {
       beg[q] = b0;
       len[q] = own ? b1 - b0 : 0;
       wmax[q] = wave_max(len[q]);
+      const int last = imax(nnz - 1, 0);
 #pragma unroll
       for (int j = 0; j < MAXNNZ; ++j) {
-        const int idx = imax(imin(b0 + j, nnz - 1), 0);  // clamped: always a valid address
-        const int cj = nnz > 0 ? col[idx] : 0;
-        const float vj = nnz > 0 ? val[idx] : 0.f;
+        const int idx = imin(b0 + j, last);  // clamped: always a valid address (nnz >= 1)
+        const int cj = col[idx];
+        const float vj = val[idx];
         const bool in = j < len[q];
-        c[q][j] = in ? cj : 0;  // padding gathers vertex 0 (always in range)
+        c[q][j] = in ? cj : M;
         v[q][j] = in ? vj : 0.f;
       }
     }
@@ -97,11 +100,10 @@ struct RowRegs {
 #pragma clang fp contract(off)
     float g[MAXNNZ];
 #pragma unroll
-    for (int j = 0; j < MAXNNZ; ++j) g[j] = (j < wmax[q]) ? T[c[q][j]] : 0.f;  // LDS gathers
+    for (int j = 0; j < MAXNNZ; ++j) g[j] = T[c[q][j]];  // independent LDS gathers
     float a = 0.f;
 #pragma unroll
-    for (int j = 0; j < MAXNNZ; ++j)
-      if (j < len[q]) a = a + v[q][j] * g[j];
+    for (int j = 0; j < MAXNNZ; ++j) a = a + v[q][j] * g[j];
     if (wmax[q] > MAXNNZ)  // rows longer than MAXNNZ (rare): global CSR tail
       for (int j = MAXNNZ; j < len[q]; ++j) a = a + val[beg[q] + j] * T[col[beg[q] + j]];
     return a;
@@ -113,7 +115,8 @@ struct RowRegs {
 // ---------------------------------------------------------------------------
 template <int RPT, int MAXNNZ, int NT>
 __global__ __launch_bounds__(kT) void cheb_fwd_resident(
-    int M, int Fin, int K, int Fout, int Mp, int stage, int dbg, const int* __restrict__ rowptr,
+    int M, int Fin, int K, int Fout, int Mp, int stage, int dbg, int nnz,
+    const int* __restrict__ rowptr,
     const int* __restrict__ col, const float* __restrict__ val, const float* __restrict__ x,
     const float* __restrict__ W, float* __restrict__ basis, float* __restrict__ y) {
 #pragma clang fp contract(off)
@@ -133,13 +136,14 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
   float* s_B = reinterpret_cast<float*>(smem + off);  // [M][FinK] (stage only)
 
   RowRegs<RPT, MAXNNZ> rows;
-  rows.load(tid, M, rowptr, col, val);
+  rows.load(tid, M, nnz, rowptr, col, val);
   for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = W ? W[i] : 0.f;
   const float* xn = x + size_t(n) * M * Fin;
   for (int i = tid; i < M * Fin; i += kT) {
     const int m = i / Fin, fin = i - m * Fin;
     s_T[fin * Mp + m] = xn[i];  // slot 0 = T_0
   }
+  for (int i = tid; i < 3 * Fin; i += kT) s_T[i * Mp + M] = 0.f;  // padding-gather zero words
   __syncthreads();
   if (dbg & 16) return;
 
@@ -175,13 +179,8 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
           float a = 0.f;
           if (kv && m < M) {
             a = Ts[m];
-            if (keep_basis) {
-              const int e = m * FinK + fin * K + kk;
-              if (stage)
-                s_B[e] = a;  // banks (25*li + kk) mod 32: conflict-free for odd FinK
-              else
-                basis_n[e] = a;
-            }
+            // banks (FinK*li + kk) mod 32: conflict-free for odd FinK
+            if (keep_basis) s_B[m * FinK + fin * K + kk] = a;
           }
           if (!(dbg & 4)) {
 #pragma unroll
@@ -192,8 +191,13 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
     }
   };
 
+  // diagnostic build only (dbg & 32): s_memtime stamps of block 0 / wave 0 into y
+  const bool stamp = (dbg & 32) && n == 0 && tid == 0 && y;
+  const long long t0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
+
   for (int k = 1; k < K; ++k) {
     if ((k & 1) == 0) mfma_pair((k - 2) >> 1);
+    if (stamp) y[2 * k] = float(__builtin_amdgcn_s_memtime() - t0);
     const int cur = k % 3, prv = (k - 1) % 3, prv2 = (k + 1) % 3;  // (k-2) mod 3 == (k+1) mod 3
     for (int fin = 0; fin < Fin; ++fin) {
       const float* Tp = s_T + (prv * Fin + fin) * Mp;
@@ -208,11 +212,14 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
         }
       }
     }
+    if (stamp) y[2 * k + 1] = float(__builtin_amdgcn_s_memtime() - t0);
     __syncthreads();
   }
   mfma_pair((K - 1) >> 1);  // the last (possibly half-empty) pair
+  if (stamp) y[0] = float(__builtin_amdgcn_s_memtime() - t0);
+  if (dbg & 32) return;
 
-  if (keep_basis && stage) {
+  if (keep_basis) {
     __syncthreads();
     const int total = M * FinK;
     if ((reinterpret_cast<uintptr_t>(basis_n) & 15) == 0) {
@@ -247,14 +254,13 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
 }
 
 // ---------------------------------------------------------------------------
-// Backward
+// Backward (dx only; dW = basis^T dy runs concurrently in k_dw_slabs)
 // ---------------------------------------------------------------------------
 template <int RPT, int MAXNNZ>
 __global__ __launch_bounds__(kT) void cheb_bwd_resident(
-    int M, int Fin, int K, int Fout, int Mp, int dbg, const int* __restrict__ trowptr,
+    int M, int Fin, int K, int Fout, int Mp, int dbg, int nnz, const int* __restrict__ trowptr,
     const int* __restrict__ tcol, const float* __restrict__ tval, const float* __restrict__ dy,
-    const float* __restrict__ basis, const float* __restrict__ W, float* __restrict__ dx,
-    float* __restrict__ dw_slab) {
+    const float* __restrict__ W, float* __restrict__ dx) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int n = blockIdx.x;
@@ -264,57 +270,99 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(
   const int h = lane >> 5, li = lane & 31;
   const int FinK = Fin * K;
 
-  const size_t dbytes = size_t(FinK) * Mp * 4;
-  constexpr size_t kScratch = size_t(kWaves) * 32 * 32 * 4;
-  float* s_D = reinterpret_cast<float*>(smem);  // [FinK][Mp], later dW scratch [16][32][32]
-  size_t off = align16(dbytes > kScratch ? dbytes : kScratch);
+  float* s_D = reinterpret_cast<float*>(smem);  // [FinK][Mp]
+  size_t off = align16(size_t(FinK) * Mp * 4);
   float* s_G = reinterpret_cast<float*>(smem + off);  // [3][Fin][Mp]
   off = align16(off + size_t(3) * Fin * Mp * 4);
   float* s_W = reinterpret_cast<float*>(smem + off);  // [FinK][Fout]
 
+  const float* dyn = dy + size_t(n) * M * Fout;
+  const int mtiles = (M + 31) >> 5, jtiles = (FinK + 31) >> 5;
+  const int ns = (Fout + 1) >> 1;  // lane half h owns f in [h*ns, h*ns + ns)
+  // Fast Phase-A operand path (config B/E shapes): each wave's <= 2 dy tiles
+  // are loaded as float4 at kernel entry, so their HBM latency overlaps the
+  // CSR / W prologue instead of trailing it.
+  const bool fastA =
+      RPT == 1 && mtiles <= 2 * kWaves && jtiles == 1 && Fout <= 32 && (Fout & 7) == 0;
+  float4 av[2][4];
+  if constexpr (RPT == 1) if (fastA) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int m = imin((wave + t * kWaves) * 32 + li, M - 1);
+      const float4* row = reinterpret_cast<const float4*>(dyn + size_t(m) * Fout + h * ns);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) av[t][c] = row[imin(c, (ns >> 2) - 1)];
+    }
+  }
+
   RowRegs<RPT, MAXNNZ> rows;
-  rows.load(tid, M, trowptr, tcol, tval);
+  rows.load(tid, M, nnz, trowptr, tcol, tval);
   for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = W[i];
+  for (int i = tid; i < 3 * Fin; i += kT) s_G[i * Mp + M] = 0.f;  // padding-gather zero words
   __syncthreads();
   if (dbg & 16) return;
 
-  const float* dyn = dy + size_t(n) * M * Fout;
-  const float* bn = basis + size_t(n) * M * FinK;
-
-  // A. dBasis = dy W^T  (rows m, cols j, inner f; lane half h owns f in [h*ns, h*ns+ns))
+  // A. dBasis = dy W^T  (rows m, cols j = fin*K + k, inner f) on MFMA into LDS
   if (!(dbg & 1)) {
-    const int mtiles = (M + 31) >> 5, jtiles = (FinK + 31) >> 5;
-    const int ns = (Fout + 1) >> 1;
-    for (int task = wave; task < mtiles * jtiles; task += kWaves) {
-      const int mt = task / jtiles, jt = task - mt * jtiles;
-      const int m = mt * 32 + li, j = jt * 32 + li;
-      const bool mv = m < M, jv = j < FinK;
-      const float* dyrow = dyn + size_t(imin(m, M - 1)) * Fout;
-      const float* wrow = s_W + imin(j, FinK - 1) * Fout;
-      f32x16 acc;
+    if (RPT == 1 && fastA) {
+      const int j = li;
+      const bool jv = j < FinK;
+      const float* wrow = s_W + imin(j, FinK - 1) * Fout + h * ns;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int s0 = 0; s0 < ns; s0 += 8) {
-        float a[8], b[8];
+      for (int t = 0; t < 2; ++t) {
+        const int mt = wave + t * kWaves;
+        if (mt < mtiles) {
+          const bool mv = mt * 32 + li < M;
+          f32x16 acc;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {  // 8 independent loads in flight
-          const int f = h * ns + s0 + u;
-          const int fc = imin(f, Fout - 1);
-          a[u] = dyrow[fc];
-          b[u] = wrow[fc];
-        }
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int f = h * ns + s0 + u;
-          const bool fv = (s0 + u) < ns && f < Fout;
-          acc = mfma32((mv && fv) ? a[u] : 0.f, (jv && fv) ? b[u] : 0.f, acc);
+          for (int s = 0; s < 16; ++s) {
+            if (s < ns) {
+              const float a = av[t][s >> 2][s & 3];
+              const float b = wrow[s];
+              acc = mfma32(mv ? a : 0.f, jv ? b : 0.f, acc);
+            }
+          }
+          if (jv) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              if (mm < M) s_D[j * Mp + mm] = acc[r];
+            }
+          }
         }
       }
-      if (jv) {
+    } else {
+      for (int task = wave; task < mtiles * jtiles; task += kWaves) {
+        const int mt = task / jtiles, jt = task - mt * jtiles;
+        const int m = mt * 32 + li, j = jt * 32 + li;
+        const bool mv = m < M, jv = j < FinK;
+        const float* dyrow = dyn + size_t(imin(m, M - 1)) * Fout;
+        const float* wrow = s_W + imin(j, FinK - 1) * Fout;
+        f32x16 acc;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (mm < M) s_D[j * Mp + mm] = acc[r];
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        for (int s0 = 0; s0 < ns; s0 += 8) {
+          float a[8], b[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {  // 8 independent loads in flight
+            const int fc = imin(h * ns + s0 + u, Fout - 1);
+            a[u] = dyrow[fc];
+            b[u] = wrow[fc];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const bool fv = (s0 + u) < ns && (h * ns + s0 + u) < Fout;
+            acc = mfma32((mv && fv) ? a[u] : 0.f, (jv && fv) ? b[u] : 0.f, acc);
+          }
+        }
+        if (jv) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (mm < M) s_D[j * Mp + mm] = acc[r];
+          }
         }
       }
     }
@@ -348,53 +396,6 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(
     }
     if (k > 0) __syncthreads();
   }
-
-  // C. dW partial = basis^T dy (rows j, cols f, inner m split over the 16 waves)
-  if (!(dbg & 4)) {
-    const int jtl = (FinK + 31) >> 5, ftl = (Fout + 31) >> 5;
-    const int chunk = (((M + kWaves - 1) / kWaves) + 1) & ~1;
-    const int mbeg = wave * chunk;
-    const int mend = imin(mbeg + chunk, M);
-    float* scratch = s_D;  // [16][32][32]
-    for (int task = 0; task < jtl * ftl; ++task) {
-      const int jt = task / ftl, ft = task - jt * ftl;
-      const int j = jt * 32 + li, f = ft * 32 + li;
-      const bool jv = j < FinK, fv = f < Fout;
-      const int jc = imin(j, FinK - 1), fc = imin(f, Fout - 1);
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      for (int mm0 = mbeg; mm0 < mend; mm0 += 16) {
-        float a[8], b[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {  // 16 independent loads in flight
-          const int mc = imin(mm0 + 2 * u + h, M - 1);
-          a[u] = bn[size_t(mc) * FinK + jc];
-          b[u] = dyn[size_t(mc) * Fout + fc];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const bool mv = (mm0 + 2 * u + h) < mend;
-          acc = mfma32((mv && jv) ? a[u] : 0.f, (mv && fv) ? b[u] : 0.f, acc);
-        }
-      }
-      __syncthreads();  // s_D free (phase B done) / previous task's readers done
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        scratch[(wave * 32 + row) * 32 + li] = acc[r];
-      }
-      __syncthreads();
-      for (int e = tid; e < 1024; e += kT) {
-        const int row = e >> 5, cc = e & 31;
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) s = s + scratch[(w * 32 + row) * 32 + cc];
-        const int jj = jt * 32 + row, ff = ft * 32 + cc;
-        if (jj < FinK && ff < Fout) dw_slab[(size_t(n) * FinK + jj) * Fout + ff] = s;
-      }
-    }
-  }
 }
 
 template <typename Kern>
@@ -410,7 +411,7 @@ hipError_t launch_fwd_t(const ResidentGeom& g, int N, int M, int Fin, int K, int
   static hipError_t attr = allow_big_lds(&cheb_fwd_resident<RPT, MAXNNZ, NT>);
   if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL((cheb_fwd_resident<RPT, MAXNNZ, NT>), dim3(N), dim3(kT), g.fwd_lds, s, M, Fin,
-                     K, Fout, lds_vertex_stride(M), int(g.stage), g_debug_flags & 0xff, rowptr,
+                     K, Fout, lds_vertex_stride(M), int(g.stage), g_debug_flags & 0xff, g.nnz, rowptr,
                      col, val, x, W, basis, y);
   return hipGetLastError();
 }
@@ -418,13 +419,12 @@ hipError_t launch_fwd_t(const ResidentGeom& g, int N, int M, int Fin, int K, int
 template <int RPT, int MAXNNZ>
 hipError_t launch_bwd_t(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
                         const int* trowptr, const int* tcol, const float* tval, const float* dy,
-                        const float* basis, const float* W, float* dx, float* dw_slab,
-                        hipStream_t s) {
+                        const float* W, float* dx, hipStream_t s) {
   static hipError_t attr = allow_big_lds(&cheb_bwd_resident<RPT, MAXNNZ>);
   if (attr != hipSuccess) return attr;
   hipLaunchKernelGGL((cheb_bwd_resident<RPT, MAXNNZ>), dim3(N), dim3(kT), g.bwd_lds, s, M, Fin, K,
-                     Fout, lds_vertex_stride(M), (g_debug_flags >> 8) & 0xff, trowptr, tcol, tval,
-                     dy, basis, W, dx, dw_slab);
+                     Fout, lds_vertex_stride(M), (g_debug_flags >> 8) & 0xff, g.nnz, trowptr, tcol, tval,
+                     dy, W, dx);
   return hipGetLastError();
 }
 
@@ -436,9 +436,10 @@ int pick_maxnnz(int rpt, int max_row_nnz) {
 
 }  // namespace
 
-ResidentGeom resident_geometry(int M, int max_row_nnz, int max_row_nnzT, int Fin, int K,
+ResidentGeom resident_geometry(int M, int nnz, int max_row_nnz, int max_row_nnzT, int Fin, int K,
                                int Fout) {
   ResidentGeom g{};
+  g.nnz = nnz;
   const int Mp = lds_vertex_stride(M);
   g.rpt = (M + kT - 1) / kT;
   g.nt = (Fout + 31) / 32;
@@ -446,14 +447,12 @@ ResidentGeom resident_geometry(int M, int max_row_nnz, int max_row_nnzT, int Fin
   g.maxnnzT = pick_maxnnz(g.rpt, max_row_nnzT);
   const size_t FinK = size_t(Fin) * K;
   const size_t base = align16(FinK * Fout * 4) + align16(size_t(3) * Fin * Mp * 4);
-  const size_t staged = base + size_t(M) * FinK * 4;
-  g.stage = staged <= size_t(kLdsBytes);
-  g.fwd_lds = g.stage ? staged : base;
-  const size_t dbytes = FinK * Mp * 4;
-  const size_t scratch = size_t(kWaves) * 32 * 32 * 4;
-  g.bwd_lds = align16(dbytes > scratch ? dbytes : scratch) + align16(size_t(3) * Fin * Mp * 4) +
-              FinK * Fout * 4;
-  const bool shape_ok = M >= 1 && Fin >= 1 && K >= 1 && Fout >= 1 && g.rpt <= 2;
+  // The forward always stages the sample's basis in LDS (coalesced store at
+  // the end); a shape whose basis block does not fit takes the streaming path.
+  g.fwd_lds = base + size_t(M) * FinK * 4;
+  g.stage = true;
+  g.bwd_lds = align16(FinK * Mp * 4) + align16(size_t(3) * Fin * Mp * 4) + FinK * Fout * 4;
+  const bool shape_ok = M >= 1 && nnz >= 1 && Fin >= 1 && K >= 1 && Fout >= 1 && g.rpt <= 2;
   // RPT=2 with two Fout tiles spills hundreds of VGPRs: leave it to the streaming path
   g.fwd_ok = shape_ok && g.nt <= 2 && !(g.rpt == 2 && g.nt == 2) && g.fwd_lds <= size_t(kLdsBytes);
   g.bwd_ok = shape_ok && g.bwd_lds <= size_t(kLdsBytes);
@@ -476,12 +475,10 @@ hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin,
 
 hipError_t launch_resident_backward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
                                     const int* trowptr, const int* tcol, const float* tval,
-                                    const float* dy, const float* basis, const float* W, float* dx,
-                                    float* dw_slab, hipStream_t s) {
-#define CG_BWD(R_, Z_)                                                                  \
-  if (g.rpt == R_ && g.maxnnzT == Z_)                                                   \
-    return launch_bwd_t<R_, Z_>(g, N, M, Fin, K, Fout, trowptr, tcol, tval, dy, basis, W, \
-                                dx, dw_slab, s);
+                                    const float* dy, const float* W, float* dx, hipStream_t s) {
+#define CG_BWD(R_, Z_)                                                                     \
+  if (g.rpt == R_ && g.maxnnzT == Z_)                                                      \
+    return launch_bwd_t<R_, Z_>(g, N, M, Fin, K, Fout, trowptr, tcol, tval, dy, W, dx, s);
   CG_BWD(1, 12) CG_BWD(1, 16) CG_BWD(1, 32) CG_BWD(2, 12) CG_BWD(2, 16)
 #undef CG_BWD
   return hipErrorInvalidValue;

@@ -187,6 +187,64 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int Mg, int Ng, int Kg, const 
   }
 }
 
+// dW partial slabs: slab[z][j][f] = sum_{r in chunk z} basis[r][j] * dy[r][f]
+// over the R = N*M basis rows (j < FinK, f < Fout): a skinny TN GEMM whose
+// inner dimension is the whole batch.  Block (z, tile) = 4 waves; wave w
+// streams rows r0 + 2u + h of its quarter of chunk z (lane half h takes the
+// odd rows) straight into v_mfma_f32_32x32x2_f32 (K = 2 rows per MFMA):
+// A lane (j, h) = basis[r][j], B lane (f, h) = dy[r][f] -- each wave load
+// instruction reads two whole 4*FinK / 4*Fout-byte rows.  16 loads per lane
+// are in flight per batch; the 4 wave partials are added in a fixed order
+// through LDS, so the result is bitwise reproducible.  HBM-bound: it reads
+// basis + dy once (4*R*(FinK + Fout) bytes) and is meant to run on a side
+// stream concurrently with the latency-bound backward recurrence.
+__global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basis,
+                                                  const float* __restrict__ dy, int64_t R,
+                                                  int FinK, int Fout, int64_t rows_per_chunk,
+                                                  float* __restrict__ slab) {
+  __shared__ float part[4][32][33];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int ftl = (Fout + 31) >> 5;
+  const int jt = blockIdx.y / ftl, ft = blockIdx.y - jt * ftl;
+  const int j = jt * 32 + li, f = ft * 32 + li;
+  const bool jv = j < FinK, fv = f < Fout;
+  const int jc = jv ? j : FinK - 1, fc = fv ? f : Fout - 1;
+  const int64_t c0 = int64_t(blockIdx.x) * rows_per_chunk;
+  const int64_t c1 = (c0 + rows_per_chunk < R) ? c0 + rows_per_chunk : R;
+  const int64_t q = (((c1 - c0) + 3) / 4 + 1) & ~int64_t(1);  // even rows per wave
+  const int64_t r0 = c0 + w * q;
+  const int64_t r1 = (r0 + q < c1) ? r0 + q : c1;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int64_t rb = r0; rb < r1; rb += 16) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      int64_t rr = rb + 2 * u + h;
+      rr = rr < R ? rr : R - 1;
+      a[u] = basis[rr * FinK + jc];
+      b[u] = dy[rr * Fout + fc];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool rv = (rb + 2 * u + h) < r1;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32((rv && jv) ? a[u] : 0.f, (rv && fv) ? b[u] : 0.f,
+                                                 acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) part[w][(r & 3) + 8 * (r >> 2) + 4 * h][li] = acc[r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int row = e >> 5, col = e & 31;
+    const float s = ((part[0][row][col] + part[1][row][col]) + part[2][row][col]) + part[3][row][col];
+    const int jj = jt * 32 + row, ff = ft * 32 + col;
+    if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jj) * Fout + ff] = s;
+  }
+}
+
 // out[i] = sum_z slab[z][i] in a FIXED order (bitwise reproducible): wave w of
 // a block sums the slabs z = w, w+16, ... for 64 consecutive outputs (one
 // 256-B coalesced load per slab, 8 in flight), then the 16 partial sums are
@@ -276,6 +334,22 @@ hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, c
   else
     hipLaunchKernelGGL((k_gemm_f32<true, true>), grid, dim3(256), 0, s, Mg, Ng, Kg, A, lda, B, ldb,
                        C, ldc, kchunk);
+  return hipGetLastError();
+}
+
+int dw_chunks(int64_t R) {
+  // ~512 rows per chunk, at most 1024 chunks (slab bytes stay <= 1024*FinK*Fout*4)
+  int64_t c = (R + 511) / 512;
+  if (c > 1024) c = 1024;
+  return int(c < 1 ? 1 : c);
+}
+
+hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
+                           float* slab, hipStream_t s) {
+  const int chunks = dw_chunks(R);
+  const int64_t rpc = (R + chunks - 1) / chunks;
+  const dim3 grid(chunks, ((FinK + 31) / 32) * ((Fout + 31) / 32));
+  hipLaunchKernelGGL(k_dw_slabs, grid, dim3(256), 0, s, basis, dy, R, FinK, Fout, rpc, slab);
   return hipGetLastError();
 }
 

@@ -20,9 +20,10 @@ from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
 FWD = {"full": 0, "no_spmm": 1, "no_basis_store": 2, "no_mfma": 4, "no_y_store": 8,
        "no_stores": 2 | 8, "only_spmm": 2 | 4 | 8, "nothing": 1 | 2 | 4 | 8, "prologue": 16}
-BWD = {"full": 0, "no_phaseA": 1, "no_clenshaw_spmm": 2, "no_phaseC": 4, "only_phaseC": 1 | 2,
-       "only_A": 2 | 4, "only_B": 1 | 4, "no_reduce": 1 << 15, "prologue": 16 | (1 << 15),
-       "nothing": 1 | 2 | 4 | (1 << 15)}
+BWD = {"full": 0, "no_phaseA": 1, "no_clenshaw_spmm": 2, "no_dw": 1 << 14,
+       "only_dw": 16 | (1 << 15), "only_A": 2 | (1 << 14), "only_B": 1 | (1 << 14),
+       "no_reduce": 1 << 15, "prologue": 16 | (1 << 14) | (1 << 15),
+       "nothing": 1 | 2 | (1 << 14) | (1 << 15)}
 
 
 def main():
