@@ -39,14 +39,48 @@ struct ResidentGeom {
 };
 ResidentGeom resident_geometry(int M, int nnz, int max_row_nnz, int max_row_nnzT, int Fin, int K,
                                int Fout);
+// Register slots per row (ELL width) the resident kernels use for this graph.
+int resident_slot_width(int M, int max_row_nnz);
 
-hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                   const int* rowptr, const int* col, const float* val,
-                                   const float* x, const float* W, float* basis, float* y,
+// Device image of a sparse operand in "thread-slot" order for the resident
+// kernels (built on the host by cheb_abi.cpp::build_slots).  Slot t in
+// [0, S), S = RPT*1024, owns row[t] (-1 = idle) with len[t] entries starting
+// at CSR offset beg[t]; col/val are [width][S] (column-major, padding
+// col = M -> a zero word, val = 0); wlen[q*16 + w] is the max len over the
+// 64 slots of wave w in slot group q.
+struct SlotLayout {
+  const int* row;
+  const int* len;
+  const int* beg;
+  const int* col;
+  const float* val;
+  const int* wlen;
+  int S;
+  int width;
+};
+struct ResidentFwdArgs {
+  int M, Fin, K, Fout, Mp, dbg;
+  SlotLayout E;                        // L~
+  const int* col;                      // CSR columns / values of L~ (tails)
+  const float* val;
+  const float* x;
+  const float* W;
+  float* basis;
+  float* y;
+};
+struct ResidentBwdArgs {
+  int M, Fin, K, Fout, Mp, dbg;
+  SlotLayout E;                        // L~^T
+  const int* col;                      // CSR of L~^T (tails)
+  const float* val;
+  const float* dy;
+  const float* W;
+  float* dx;
+};
+hipError_t launch_resident_forward(const ResidentGeom& g, int N, const ResidentFwdArgs& a,
                                    hipStream_t s);
-hipError_t launch_resident_backward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                    const int* trowptr, const int* tcol, const float* tval,
-                                    const float* dy, const float* W, float* dx, hipStream_t s);
+hipError_t launch_resident_backward(const ResidentGeom& g, int N, const ResidentBwdArgs& a,
+                                    hipStream_t s);
 
 // ---- streaming path ----------------------------------------------------------
 hipError_t launch_x_to_cols(const float* x, float* T0, float* basis, int N, int M, int Fin, int K,

@@ -33,6 +33,11 @@ struct cg_plan {
   float* tval = nullptr;
   hipStream_t side = nullptr;  // dW kernel runs here, overlapped with the dx recurrence
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // thread-slot images of L~ and L~^T for the resident kernels (M <= 2048)
+  struct Slots {
+    int* buf = nullptr;  // one allocation: row | len | beg | col | val | wlen
+    cg::SlotLayout view{};
+  } slots, tslots;
 };
 
 namespace {
@@ -99,6 +104,75 @@ void transpose_csr(int32_t M, int64_t nnz, const int32_t* rp, const int32_t* ci,
     }
 }
 
+// Thread-slot ELL image of a CSR operand for the resident kernels
+// (cg_internal.h::SlotLayout).  Rows are dealt to thread slots in order of
+// decreasing length (stable), so the 64 rows of a wave have nearly equal
+// length and the kernel can skip whole gather instructions past the wave's
+// maximum; the ELL arrays are column-major so each prologue load is one
+// coalesced 256-byte wave access.
+int build_slots(cg_plan::Slots* out, int32_t M, const int32_t* rp, const int32_t* ci,
+                const float* v) {
+  constexpr int kT = cg::kResidentThreads, kW = kT / 64;
+  const int rpt = (M + kT - 1) / kT;
+  if (rpt > 2) return CG_OK;  // resident path not available: no image
+  int maxlen = 0;
+  for (int32_t r = 0; r < M; ++r) maxlen = std::max(maxlen, rp[r + 1] - rp[r]);
+  const int width = cg::resident_slot_width(M, maxlen);
+  const int S = rpt * kT;
+  std::vector<int32_t> order(static_cast<size_t>(M));
+  for (int32_t r = 0; r < M; ++r) order[size_t(r)] = r;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return (rp[a + 1] - rp[a]) > (rp[b + 1] - rp[b]);
+  });
+  // slot t = q*kT + tid: deal sorted rows tid-major inside each slot group
+  std::vector<int32_t> row(size_t(S), -1), len(size_t(S), 0), beg(size_t(S), 0);
+  std::vector<int32_t> col(size_t(width) * S, M), wlen(size_t(rpt) * kW, 0);
+  std::vector<float> val(size_t(width) * S, 0.f);
+  for (int32_t i = 0; i < M; ++i) {
+    const int32_t r = order[size_t(i)];
+    const int t = i;  // group q = i / kT, tid = i % kT
+    row[size_t(t)] = r;
+    len[size_t(t)] = rp[r + 1] - rp[r];
+    beg[size_t(t)] = rp[r];
+    for (int j = 0; j < std::min(width, len[size_t(t)]); ++j) {
+      col[size_t(j) * S + t] = ci[rp[r] + j];
+      val[size_t(j) * S + t] = v[rp[r] + j];
+    }
+    const int w = (t / kT) * kW + (t % kT) / 64;
+    wlen[size_t(w)] = std::max(wlen[size_t(w)], len[size_t(t)]);
+  }
+  const size_t n_int = 3 * size_t(S) + size_t(width) * S + size_t(width) * S + wlen.size();
+  int* d = nullptr;
+  CG_HIP(hipMalloc(reinterpret_cast<void**>(&d), n_int * 4));
+  size_t o = 0;
+  auto put = [&](const void* src, size_t count) -> int {
+    CG_HIP(hipMemcpy(d + o, src, count * 4, hipMemcpyHostToDevice));
+    o += count;
+    return CG_OK;
+  };
+  int rc = put(row.data(), row.size());
+  if (!rc) rc = put(len.data(), len.size());
+  if (!rc) rc = put(beg.data(), beg.size());
+  if (!rc) rc = put(col.data(), col.size());
+  if (!rc) rc = put(val.data(), val.size());
+  if (!rc) rc = put(wlen.data(), wlen.size());
+  if (rc) {
+    (void)hipFree(d);
+    return rc;
+  }
+  out->buf = d;
+  cg::SlotLayout& e = out->view;
+  e.S = S;
+  e.width = width;
+  e.row = d;
+  e.len = d + S;
+  e.beg = d + 2 * size_t(S);
+  e.col = d + 3 * size_t(S);
+  e.val = reinterpret_cast<const float*>(d + 3 * size_t(S) + size_t(width) * S);
+  e.wlen = d + 3 * size_t(S) + 2 * size_t(width) * S;
+  return CG_OK;
+}
+
 template <typename T>
 int upload(T** dst, const T* src, size_t count) {
   *dst = nullptr;
@@ -113,6 +187,8 @@ void free_plan(cg_plan* p) {
   void* ptrs[] = {p->rowptr, p->col, p->val, p->trowptr, p->tcol, p->tval};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
+  if (p->slots.buf) (void)hipFree(p->slots.buf);
+  if (p->tslots.buf) (void)hipFree(p->tslots.buf);
   if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
   if (p->ev_join) (void)hipEventDestroy(p->ev_join);
   if (p->side) (void)hipStreamDestroy(p->side);
@@ -264,6 +340,8 @@ int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz, const int
   if (!rc) rc = upload(&p->trowptr, trp.data(), trp.size());
   if (!rc) rc = upload(&p->tcol, tci.data(), tci.size());
   if (!rc) rc = upload(&p->tval, tv.data(), tv.size());
+  if (!rc && nnz > 0) rc = build_slots(&p->slots, M, rowptr, col, val);
+  if (!rc && nnz > 0) rc = build_slots(&p->tslots, M, trp.data(), tci.data(), tv.data());
   (void)hipSetDevice(prev);
   if (rc) {
     free_plan(p);
@@ -322,8 +400,21 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
 
   if (path == CG_PATH_RESIDENT) {
     const cg::ResidentGeom g = cg::resident_geometry(M, int(plan->nnz), plan->max_row_nnz, plan->max_row_nnzT, Fin, K, Fout);
-    CG_HIP(cg::launch_resident_forward(g, N, M, Fin, K, Fout, plan->rowptr, plan->col, plan->val,
-                                       x, y ? W : nullptr, basis, y, s));
+    cg::ResidentFwdArgs a{};
+    a.M = M;
+    a.Fin = Fin;
+    a.K = K;
+    a.Fout = Fout;
+    a.Mp = cg::lds_vertex_stride(M);
+    a.dbg = cg::g_debug_flags & 0xff;
+    a.E = plan->slots.view;
+    a.col = plan->col;
+    a.val = plan->val;
+    a.x = x;
+    a.W = y ? W : nullptr;
+    a.basis = basis;
+    a.y = y;
+    CG_HIP(cg::launch_resident_forward(g, N, a, s));
     return ok();
   }
   // streaming path
@@ -384,8 +475,20 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
     if (path == CG_PATH_RESIDENT) {
       const cg::ResidentGeom g = cg::resident_geometry(M, int(plan->nnz), plan->max_row_nnz,
                                                        plan->max_row_nnzT, Fin, K, Fout);
-      CG_HIP(cg::launch_resident_backward(g, N, M, Fin, K, Fout, plan->trowptr, plan->tcol,
-                                          plan->tval, dy, W, dx, s));
+      cg::ResidentBwdArgs a{};
+      a.M = M;
+      a.Fin = Fin;
+      a.K = K;
+      a.Fout = Fout;
+      a.Mp = cg::lds_vertex_stride(M);
+      a.dbg = (cg::g_debug_flags >> 8) & 0xff;
+      a.E = plan->tslots.view;
+      a.col = plan->tcol;
+      a.val = plan->tval;
+      a.dy = dy;
+      a.W = W;
+      a.dx = dx;
+      CG_HIP(cg::launch_resident_backward(g, N, a, s));
     } else {
       const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
       float* ring = reinterpret_cast<float*>(rest);

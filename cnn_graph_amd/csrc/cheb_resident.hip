@@ -3,37 +3,46 @@
 // One 1024-thread workgroup (16 waves, 4 per SIMD) per sample n.  The whole
 // K-step recurrence
 //   T_0 = X, T_1 = L~X, T_k = 2 L~ T_{k-1} - T_{k-2}      (lib/graph_conv.py:163-169)
-// runs on chip: each thread owns RPT rows of L~ and keeps their CSR entries
-// (column, value) in REGISTERS for the whole launch -- the sparse operand is
-// read from L2 once per workgroup -- while a 3-slot ring of vertex vectors
-// lives in LDS.  A step is one burst of independent LDS gathers per row, a
-// sequential fp32 accumulation, and one barrier.
+// runs on chip:
+//   * each thread owns RPT rows of L~ and keeps their entries in REGISTERS for
+//     the whole launch.  The host lays the sparse operand out as a padded ELL
+//     image in "thread-slot" order (cheb_abi.cpp::build_slots): rows sorted by
+//     degree so the rows of one wave have (nearly) equal length, column-major
+//     so the prologue loads are coalesced, and a per-wave max length that lets
+//     whole gather instructions be skipped;
+//   * the 3-slot ring T_{k-2}, T_{k-1}, T_k lives in LDS as [vertex][slot]
+//     (12-byte stride: consecutive vertices hit consecutive banks), and the k
+//     loop is unrolled by 6 so the ring slot of every gather is an immediate
+//     offset of the ds_read (no address arithmetic per step).
+// A step is one burst of independent LDS gathers per row, a sequential fp32
+// accumulation, one LDS store and one barrier.
 //
 // The weight contraction y = basis @ W (lib/graph_conv.py:175) is folded into
 // the recurrence: every two steps each wave feeds the pair (T_{2s}, T_{2s+1})
 // of its 32-vertex tiles to v_mfma_f32_32x32x2_f32, whose K=2 is exactly one
 // Chebyshev pair, accumulating y in registers.  The same A-operand values are
 // the basis entries: they are staged in LDS in the HBM layout of
-// lib/graph_conv.py:172 ([m][fin*K+k], a contiguous block per sample) and
-// leave with fully coalesced stores at the end (a row of that layout is only
-// complete after the last step, so streaming it earlier would write partial
-// lines -- measured 28 us of scattered 4-byte stores on config B).
+// lib/graph_conv.py:172 ([m][fin*K+k], one contiguous block per sample) and
+// leave with coalesced 16-byte stores at the end (a row of that layout is only
+// complete after the last step, so streaming it earlier writes partial lines:
+// measured 28 us of scattered 4-byte stores on config B).
 //
 // The backward kernel does, per sample:
 //   A. dBasis = dy W^T on MFMA into LDS (D[j][m], j = fin*K + k);
-//   B. the reverse (Clenshaw) recurrence over L~^T (CSR in registers)
+//   B. the reverse (Clenshaw) recurrence over L~^T with the same register /
+//      ring machinery
 //        G_{K-1} = D_{K-1};  G_k = D_k + 2 L~^T G_{k+1} - G_{k+2};  G_0 = D_0 + L~^T G_1 - G_2
 //      writing dx = G_0 straight to HBM.
-// dW = basis^T dy is not computed here: it is HBM-streaming work that the C
-// ABI launches (k_dw_slabs) on a side stream to overlap this latency-bound kernel.
-// All global loads are issued unconditionally from clamped addresses and
-// masked afterwards, so hipcc does not branch around each load (one vmcnt(0)
-// per element, guide §5 "Three .s-level traps" (c)).
+// dW = basis^T dy is HBM-streaming work done by k_dw_slabs (cheb_stream.hip).
 //
-// Numerics: each row accumulates sequentially from 0 in CSR order with one
+// Numerics: each row accumulates sequentially from +0 in CSR order with one
 // rounding per product and per add (fp contraction OFF) -- the order of scipy
 // csr_matvecs / TF SparseTensorDenseMatMul -- so the basis is bit-exact to
-// lib/graph.py::chebyshev.  MFMA f32 is an exact fp32 fma chain.
+// lib/graph.py::chebyshev.  Padding entries gather a word kept at 0 with
+// weight 0 and add an exact +0 (the running sum is never -0).  MFMA f32 is an
+// exact fp32 fma chain.
+#include <type_traits>
+
 #include "cg_internal.h"
 
 namespace cg {
@@ -42,70 +51,61 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kT = kResidentThreads;  // 1024
 constexpr int kWaves = kT / 64;       // 16
+template <int V>
+using I = std::integral_constant<int, V>;
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
-
 __device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
-__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+__device__ __forceinline__ float lds_f(const char* p) { return *reinterpret_cast<const float*>(p); }
+__device__ __forceinline__ void lds_st(char* p, float v) { *reinterpret_cast<float*>(p) = v; }
 
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = imax(v, __shfl_xor(v, o));
-  return __builtin_amdgcn_readfirstlane(v);
-}
-
-// Register-resident CSR rows of one thread: rows tid, tid + kT, ...
-// Padding slots (j >= row length) gather vertex index M of the LDS vector,
-// a word that is kept at 0 (the stride Mp > M), with value 0: they add an
-// exact +0 to the running sum (which starts at +0 and so is never -0), so
-// the accumulation needs no per-lane predicate and stays bit-exact.
+// Registers of the rows a thread owns (thread slot t = q*kT + tid).
 template <int RPT, int MAXNNZ>
 struct RowRegs {
-  int beg[RPT];
+  int row[RPT];    // vertex, or -1 for an idle slot
+  int rb[RPT];     // row * 12: byte offset of the vertex in a [Mp][3] ring block
+  int beg[RPT];    // CSR offset of the row (tail loop for rows longer than MAXNNZ)
   int len[RPT];
-  int wmax[RPT];  // wave-uniform max(len) over the wave's rows (tail loop trigger)
-  int c[RPT][MAXNNZ];
+  int wl[RPT];     // wave-uniform max row length of the slot group
+  int ca[RPT][MAXNNZ];  // gather byte offsets (column * 12); padding -> zero word
   float v[RPT][MAXNNZ];
 
-  __device__ __forceinline__ void load(int tid, int M, int nnz, const int* __restrict__ rowptr,
-                                       const int* __restrict__ col,
-                                       const float* __restrict__ val) {
+  __device__ __forceinline__ void load(const SlotLayout& E, int tid, int wave) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-      const int r = imin(tid + q * kT, M - 1);
-      const bool own = (tid + q * kT) < M;
-      const int b0 = rowptr[r], b1 = rowptr[r + 1];
-      beg[q] = b0;
-      len[q] = own ? b1 - b0 : 0;
-      wmax[q] = wave_max(len[q]);
-      const int last = imax(nnz - 1, 0);
+      const int t = q * kT + tid;
+      row[q] = E.row[t];
+      len[q] = E.len[t];
+      beg[q] = E.beg[t];
+      wl[q] = E.wlen[q * kWaves + wave];  // uniform index: scalar load
+      rb[q] = row[q] * 12;
 #pragma unroll
       for (int j = 0; j < MAXNNZ; ++j) {
-        const int idx = imin(b0 + j, last);  // clamped: always a valid address (nnz >= 1)
-        const int cj = col[idx];
-        const float vj = val[idx];
-        const bool in = j < len[q];
-        c[q][j] = in ? cj : M;
-        v[q][j] = in ? vj : 0.f;
+        ca[q][j] = E.col[j * E.S + t] * 12;
+        v[q][j] = E.val[j * E.S + t];
       }
     }
   }
 
-  // sum_{j in row, CSR order} v_j * T[c_j]   (sequential, no contraction)
-  __device__ __forceinline__ float dot(int q, const float* __restrict__ T,
+  // sum_{j in row, CSR order} v_j * T[c_j][SLOT]   (sequential, no contraction)
+  template <int SLOT>
+  __device__ __forceinline__ float dot(int q, const char* __restrict__ Tb,
                                        const int* __restrict__ col,
                                        const float* __restrict__ val) const {
 #pragma clang fp contract(off)
+    const char* base = Tb + SLOT * 4;
     float g[MAXNNZ];
 #pragma unroll
-    for (int j = 0; j < MAXNNZ; ++j) g[j] = T[c[q][j]];  // independent LDS gathers
+    for (int j = 0; j < MAXNNZ; ++j) g[j] = (j < wl[q]) ? lds_f(base + ca[q][j]) : 0.f;
     float a = 0.f;
 #pragma unroll
-    for (int j = 0; j < MAXNNZ; ++j) a = a + v[q][j] * g[j];
-    if (wmax[q] > MAXNNZ)  // rows longer than MAXNNZ (rare): global CSR tail
-      for (int j = MAXNNZ; j < len[q]; ++j) a = a + val[beg[q] + j] * T[col[beg[q] + j]];
+    for (int j = 0; j < MAXNNZ; ++j)
+      if (j < wl[q]) a = a + v[q][j] * g[j];
+    if (wl[q] > MAXNNZ)  // rows longer than MAXNNZ (rare): CSR tail from L2
+      for (int j = MAXNNZ; j < len[q]; ++j)
+        a = a + val[beg[q] + j] * lds_f(base + col[beg[q] + j] * 12);
     return a;
   }
 };
@@ -113,37 +113,37 @@ struct RowRegs {
 // ---------------------------------------------------------------------------
 // Forward
 // ---------------------------------------------------------------------------
-template <int RPT, int MAXNNZ, int NT>
-__global__ __launch_bounds__(kT) void cheb_fwd_resident(
-    int M, int Fin, int K, int Fout, int Mp, int stage, int dbg, int nnz,
-    const int* __restrict__ rowptr,
-    const int* __restrict__ col, const float* __restrict__ val, const float* __restrict__ x,
-    const float* __restrict__ W, float* __restrict__ basis, float* __restrict__ y) {
+template <int RPT, int MAXNNZ, int NT, bool FIN1>
+__global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
 #pragma clang fp contract(off)
   constexpr int MT = 2 * RPT;  // 32-vertex tiles per wave: ceil(M/32)/16 <= 2*RPT
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int M = A.M, K = A.K, Fout = A.Fout, Mp = A.Mp, dbg = A.dbg;
+  const int Fin = FIN1 ? 1 : A.Fin;
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, li = lane & 31;
   const int FinK = Fin * K;
+  const int slab = Mp * 12;  // bytes of one [Mp][3] ring block (one fin)
 
   float* s_W = reinterpret_cast<float*>(smem);
   size_t off = align16(size_t(FinK) * Fout * 4);
-  float* s_T = reinterpret_cast<float*>(smem + off);  // [3][Fin][Mp]
-  off = align16(off + size_t(3) * Fin * Mp * 4);
-  float* s_B = reinterpret_cast<float*>(smem + off);  // [M][FinK] (stage only)
+  char* s_T = smem + off;  // [Fin][Mp][3] floats
+  off = align16(off + size_t(Fin) * slab);
+  float* s_B = reinterpret_cast<float*>(smem + off);  // [M][FinK]
 
   RowRegs<RPT, MAXNNZ> rows;
-  rows.load(tid, M, nnz, rowptr, col, val);
-  for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = W ? W[i] : 0.f;
-  const float* xn = x + size_t(n) * M * Fin;
+  rows.load(A.E, tid, wave);
+  for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = A.W ? A.W[i] : 0.f;
+  const float* xn = A.x + size_t(n) * M * Fin;
   for (int i = tid; i < M * Fin; i += kT) {
     const int m = i / Fin, fin = i - m * Fin;
-    s_T[fin * Mp + m] = xn[i];  // slot 0 = T_0
+    lds_st(s_T + fin * slab + m * 12, xn[i]);  // slot 0 = T_0
   }
-  for (int i = tid; i < 3 * Fin; i += kT) s_T[i * Mp + M] = 0.f;  // padding-gather zero words
+  for (int i = tid; i < 3 * Fin; i += kT)  // zero words gathered by padding entries
+    lds_st(s_T + (i / 3) * slab + M * 12 + (i % 3) * 4, 0.f);
   __syncthreads();
   if (dbg & 16) return;
 
@@ -155,14 +155,13 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
     for (int q = 0; q < NT; ++q)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][q][r] = 0.f;
+  const bool keep_basis = A.basis && !(dbg & 2);
 
-  float* basis_n = basis ? basis + size_t(n) * M * FinK : nullptr;
-  const bool keep_basis = basis_n && !(dbg & 2);
-
+  // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA; stage the basis.
   auto mfma_pair = [&](int s) {
     const int kk = 2 * s + h;
     const bool kv = kk < K;
-    const int slot = kk % 3;
+    const int soff = (kk % 3) * 4;
     for (int fin = 0; fin < Fin; ++fin) {
       float b[NT];
 #pragma unroll
@@ -170,7 +169,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
         const int f = q * 32 + li;
         b[q] = (kv && f < Fout) ? s_W[(fin * K + kk) * Fout + f] : 0.f;
       }
-      const float* Ts = s_T + (slot * Fin + fin) * Mp;
+      const char* Tb = s_T + fin * slab + soff;
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const int tile = wave + t * kWaves;
@@ -178,9 +177,8 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
           const int m = tile * 32 + li;
           float a = 0.f;
           if (kv && m < M) {
-            a = Ts[m];
-            // banks (FinK*li + kk) mod 32: conflict-free for odd FinK
-            if (keep_basis) s_B[m * FinK + fin * K + kk] = a;
+            a = lds_f(Tb + m * 12);
+            if (keep_basis) s_B[m * FinK + fin * K + kk] = a;  // banks (FinK*li+kk) mod 32
           }
           if (!(dbg & 4)) {
 #pragma unroll
@@ -191,36 +189,39 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
     }
   };
 
-  // diagnostic build only (dbg & 32): s_memtime stamps of block 0 / wave 0 into y
-  const bool stamp = (dbg & 32) && n == 0 && tid == 0 && y;
-  const long long t0 = stamp ? __builtin_amdgcn_s_memtime() : 0;
-
-  for (int k = 1; k < K; ++k) {
-    if ((k & 1) == 0) mfma_pair((k - 2) >> 1);
-    if (stamp) y[2 * k] = float(__builtin_amdgcn_s_memtime() - t0);
-    const int cur = k % 3, prv = (k - 1) % 3, prv2 = (k + 1) % 3;  // (k-2) mod 3 == (k+1) mod 3
+  // One recurrence step k with compile-time ring slots (slot(k) = k mod 3).
+  auto step = [&](auto cur_c, auto prv_c, auto prv2_c, int k) {
+    constexpr int CUR = decltype(cur_c)::value, PRV = decltype(prv_c)::value,
+                  PRV2 = decltype(prv2_c)::value;
     for (int fin = 0; fin < Fin; ++fin) {
-      const float* Tp = s_T + (prv * Fin + fin) * Mp;
-      const float* Tp2 = s_T + (prv2 * Fin + fin) * Mp;
-      float* To = s_T + (cur * Fin + fin) * Mp;
+      char* Tb = s_T + (FIN1 ? 0 : fin * slab);
 #pragma unroll
       for (int q = 0; q < RPT; ++q) {
-        const int r = tid + q * kT;
-        if (r < M) {
-          const float a = (dbg & 1) ? Tp[r] : rows.dot(q, Tp, col, val);
-          To[r] = (k == 1) ? a : (2.f * a - Tp2[r]);
+        if (rows.row[q] >= 0) {
+          char* rp = Tb + rows.rb[q];
+          const float a = (dbg & 1) ? lds_f(rp + PRV * 4)
+                                    : rows.template dot<PRV>(q, Tb, A.col, A.val);
+          const float o = (k == 1) ? a : (2.f * a - lds_f(rp + PRV2 * 4));
+          lds_st(rp + CUR * 4, o);
         }
       }
     }
-    if (stamp) y[2 * k + 1] = float(__builtin_amdgcn_s_memtime() - t0);
     __syncthreads();
+  };
+
+  for (int k = 1; k < K; k += 6) {  // k = 1 (mod 6): slots cur/prv/prv2 = 1/0/2
+    step(I<1>(), I<0>(), I<2>(), k);
+    if (k + 1 < K) { mfma_pair((k - 1) >> 1); step(I<2>(), I<1>(), I<0>(), k + 1); }
+    if (k + 2 < K) step(I<0>(), I<2>(), I<1>(), k + 2);
+    if (k + 3 < K) { mfma_pair((k + 1) >> 1); step(I<1>(), I<0>(), I<2>(), k + 3); }
+    if (k + 4 < K) step(I<2>(), I<1>(), I<0>(), k + 4);
+    if (k + 5 < K) { mfma_pair((k + 3) >> 1); step(I<0>(), I<2>(), I<1>(), k + 5); }
   }
   mfma_pair((K - 1) >> 1);  // the last (possibly half-empty) pair
-  if (stamp) y[0] = float(__builtin_amdgcn_s_memtime() - t0);
-  if (dbg & 32) return;
 
   if (keep_basis) {
     __syncthreads();
+    float* basis_n = A.basis + size_t(n) * M * FinK;
     const int total = M * FinK;
     if ((reinterpret_cast<uintptr_t>(basis_n) & 15) == 0) {
       const int n4 = total >> 2;
@@ -233,8 +234,8 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
     }
   }
 
-  if (y && !(dbg & 8)) {
-    float* yn = y + size_t(n) * M * Fout;
+  if (A.y && !(dbg & 8)) {
+    float* yn = A.y + size_t(n) * M * Fout;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int tile = wave + t * kWaves;
@@ -254,60 +255,73 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(
 }
 
 // ---------------------------------------------------------------------------
-// Backward (dx only; dW = basis^T dy runs concurrently in k_dw_slabs)
+// Backward (dx)
 // ---------------------------------------------------------------------------
-template <int RPT, int MAXNNZ>
-__global__ __launch_bounds__(kT) void cheb_bwd_resident(
-    int M, int Fin, int K, int Fout, int Mp, int dbg, int nnz, const int* __restrict__ trowptr,
-    const int* __restrict__ tcol, const float* __restrict__ tval, const float* __restrict__ dy,
-    const float* __restrict__ W, float* __restrict__ dx) {
+template <int RPT, int MAXNNZ, bool FIN1>
+__global__ __launch_bounds__(kT) void cheb_bwd_resident(ResidentBwdArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int M = A.M, K = A.K, Fout = A.Fout, Mp = A.Mp, dbg = A.dbg;
+  const int Fin = FIN1 ? 1 : A.Fin;
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, li = lane & 31;
   const int FinK = Fin * K;
+  const int slab = Mp * 12;
+  const int ws = Fout + 1;  // padded W row stride: the transposed B-operand read is conflict-free
 
   float* s_D = reinterpret_cast<float*>(smem);  // [FinK][Mp]
   size_t off = align16(size_t(FinK) * Mp * 4);
-  float* s_G = reinterpret_cast<float*>(smem + off);  // [3][Fin][Mp]
-  off = align16(off + size_t(3) * Fin * Mp * 4);
-  float* s_W = reinterpret_cast<float*>(smem + off);  // [FinK][Fout]
+  char* s_G = smem + off;  // [Fin][Mp][3]
+  off = align16(off + size_t(Fin) * slab);
+  float* s_W = reinterpret_cast<float*>(smem + off);  // [FinK][Fout+1]
 
-  const float* dyn = dy + size_t(n) * M * Fout;
+  const float* dyn = A.dy + size_t(n) * M * Fout;
   const int mtiles = (M + 31) >> 5, jtiles = (FinK + 31) >> 5;
   const int ns = (Fout + 1) >> 1;  // lane half h owns f in [h*ns, h*ns + ns)
   // Fast Phase-A operand path (config B/E shapes): each wave's <= 2 dy tiles
   // are loaded as float4 at kernel entry, so their HBM latency overlaps the
-  // CSR / W prologue instead of trailing it.
+  // register / W prologue.
   const bool fastA =
       RPT == 1 && mtiles <= 2 * kWaves && jtiles == 1 && Fout <= 32 && (Fout & 7) == 0;
   float4 av[2][4];
-  if constexpr (RPT == 1) if (fastA) {
+  if constexpr (RPT == 1) {
+    if (fastA) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int m = imin((wave + t * kWaves) * 32 + li, M - 1);
-      const float4* row = reinterpret_cast<const float4*>(dyn + size_t(m) * Fout + h * ns);
+      for (int t = 0; t < 2; ++t) {
+        const int m = imin((wave + t * kWaves) * 32 + li, M - 1);
+        const float4* rowp = reinterpret_cast<const float4*>(dyn + size_t(m) * Fout + h * ns);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) av[t][c] = row[imin(c, (ns >> 2) - 1)];
+        for (int c = 0; c < 4; ++c) av[t][c] = rowp[imin(c, (ns >> 2) - 1)];
+      }
     }
   }
 
   RowRegs<RPT, MAXNNZ> rows;
-  rows.load(tid, M, nnz, trowptr, tcol, tval);
-  for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = W[i];
-  for (int i = tid; i < 3 * Fin; i += kT) s_G[i * Mp + M] = 0.f;  // padding-gather zero words
+  rows.load(A.E, tid, wave);
+  for (int i = tid; i < FinK * Fout; i += kT) s_W[(i / Fout) * ws + (i % Fout)] = A.W[i];
+  for (int i = tid; i < 3 * Fin; i += kT)
+    lds_st(s_G + (i / 3) * slab + M * 12 + (i % 3) * 4, 0.f);
   __syncthreads();
   if (dbg & 16) return;
 
   // A. dBasis = dy W^T  (rows m, cols j = fin*K + k, inner f) on MFMA into LDS
+  auto store_D = [&](const f32x16& acc, int mt, int j) {
+    if (j < FinK) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (mm < M) s_D[j * Mp + mm] = acc[r];
+      }
+    }
+  };
   if (!(dbg & 1)) {
     if (RPT == 1 && fastA) {
       const int j = li;
       const bool jv = j < FinK;
-      const float* wrow = s_W + imin(j, FinK - 1) * Fout + h * ns;
+      const float* wrow = s_W + imin(j, FinK - 1) * ws + h * ns;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int mt = wave + t * kWaves;
@@ -318,19 +332,9 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(
           for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
           for (int s = 0; s < 16; ++s) {
-            if (s < ns) {
-              const float a = av[t][s >> 2][s & 3];
-              const float b = wrow[s];
-              acc = mfma32(mv ? a : 0.f, jv ? b : 0.f, acc);
-            }
+            if (s < ns) acc = mfma32(mv ? av[t][s >> 2][s & 3] : 0.f, jv ? wrow[s] : 0.f, acc);
           }
-          if (jv) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              if (mm < M) s_D[j * Mp + mm] = acc[r];
-            }
-          }
+          store_D(acc, mt, j);
         }
       }
     } else {
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(
         const int m = mt * 32 + li, j = jt * 32 + li;
         const bool mv = m < M, jv = j < FinK;
         const float* dyrow = dyn + size_t(imin(m, M - 1)) * Fout;
-        const float* wrow = s_W + imin(j, FinK - 1) * Fout;
+        const float* wrow = s_W + imin(j, FinK - 1) * ws;
         f32x16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -357,44 +361,45 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(
             acc = mfma32((mv && fv) ? a[u] : 0.f, (jv && fv) ? b[u] : 0.f, acc);
           }
         }
-        if (jv) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (mm < M) s_D[j * Mp + mm] = acc[r];
-          }
-        }
+        store_D(acc, mt, j);
       }
     }
   }
   __syncthreads();
 
-  // B. reverse recurrence over L~^T
-  for (int k = K - 1; k >= 0; --k) {
-    const int cur = k % 3, nx1 = (k + 1) % 3, nx2 = (k + 2) % 3;
-    const bool has1 = (k + 1) <= (K - 1), has2 = (k + 2) <= (K - 1);
+  // B. reverse recurrence over L~^T; step i = K-1-k writes ring slot i mod 3.
+  auto step = [&](auto cur_c, auto nx1_c, auto nx2_c, int i) {
+    constexpr int CUR = decltype(cur_c)::value, NX1 = decltype(nx1_c)::value,
+                  NX2 = decltype(nx2_c)::value;
+    const int k = K - 1 - i;
     const float c = (k >= 1) ? 2.f : 1.f;
     for (int fin = 0; fin < Fin; ++fin) {
-      const float* G1 = s_G + (nx1 * Fin + fin) * Mp;
-      const float* G2 = s_G + (nx2 * Fin + fin) * Mp;
-      float* Go = s_G + (cur * Fin + fin) * Mp;
+      char* Gb = s_G + (FIN1 ? 0 : fin * slab);
       const float* Dk = s_D + (fin * K + k) * Mp;
 #pragma unroll
       for (int q = 0; q < RPT; ++q) {
-        const int r = tid + q * kT;
-        if (r < M) {
-          const float a = has1 ? ((dbg & 2) ? G1[r] : rows.dot(q, G1, tcol, tval)) : 0.f;
+        const int r = rows.row[q];
+        if (r >= 0) {
+          char* rp = Gb + rows.rb[q];
+          const float a = (i >= 1) ? ((dbg & 2) ? lds_f(rp + NX1 * 4)
+                                                : rows.template dot<NX1>(q, Gb, A.col, A.val))
+                                   : 0.f;
           float g = Dk[r] + c * a;
-          if (has2) g = g - G2[r];
+          if (i >= 2) g = g - lds_f(rp + NX2 * 4);
           if (k == 0) {
-            if (dx) dx[(size_t(n) * M + r) * Fin + fin] = g;
+            if (A.dx) A.dx[(size_t(n) * M + r) * Fin + fin] = g;
           } else {
-            Go[r] = g;
+            lds_st(rp + CUR * 4, g);
           }
         }
       }
     }
     if (k > 0) __syncthreads();
+  };
+  for (int i = 0; i < K; i += 3) {
+    step(I<0>(), I<2>(), I<1>(), i);
+    if (i + 1 < K) step(I<1>(), I<0>(), I<2>(), i + 1);
+    if (i + 2 < K) step(I<2>(), I<1>(), I<0>(), i + 2);
   }
 }
 
@@ -404,37 +409,30 @@ hipError_t allow_big_lds(Kern k) {
                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
 }
 
-template <int RPT, int MAXNNZ, int NT>
-hipError_t launch_fwd_t(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                        const int* rowptr, const int* col, const float* val, const float* x,
-                        const float* W, float* basis, float* y, hipStream_t s) {
-  static hipError_t attr = allow_big_lds(&cheb_fwd_resident<RPT, MAXNNZ, NT>);
+template <int RPT, int MAXNNZ, int NT, bool FIN1>
+hipError_t launch_fwd_t(const ResidentGeom& g, int N, const ResidentFwdArgs& a, hipStream_t s) {
+  static hipError_t attr = allow_big_lds(&cheb_fwd_resident<RPT, MAXNNZ, NT, FIN1>);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((cheb_fwd_resident<RPT, MAXNNZ, NT>), dim3(N), dim3(kT), g.fwd_lds, s, M, Fin,
-                     K, Fout, lds_vertex_stride(M), int(g.stage), g_debug_flags & 0xff, g.nnz, rowptr,
-                     col, val, x, W, basis, y);
+  hipLaunchKernelGGL((cheb_fwd_resident<RPT, MAXNNZ, NT, FIN1>), dim3(N), dim3(kT), g.fwd_lds, s,
+                     a);
   return hipGetLastError();
 }
 
-template <int RPT, int MAXNNZ>
-hipError_t launch_bwd_t(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                        const int* trowptr, const int* tcol, const float* tval, const float* dy,
-                        const float* W, float* dx, hipStream_t s) {
-  static hipError_t attr = allow_big_lds(&cheb_bwd_resident<RPT, MAXNNZ>);
+template <int RPT, int MAXNNZ, bool FIN1>
+hipError_t launch_bwd_t(const ResidentGeom& g, int N, const ResidentBwdArgs& a, hipStream_t s) {
+  static hipError_t attr = allow_big_lds(&cheb_bwd_resident<RPT, MAXNNZ, FIN1>);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((cheb_bwd_resident<RPT, MAXNNZ>), dim3(N), dim3(kT), g.bwd_lds, s, M, Fin, K,
-                     Fout, lds_vertex_stride(M), (g_debug_flags >> 8) & 0xff, g.nnz, trowptr, tcol, tval,
-                     dy, W, dx);
+  hipLaunchKernelGGL((cheb_bwd_resident<RPT, MAXNNZ, FIN1>), dim3(N), dim3(kT), g.bwd_lds, s, a);
   return hipGetLastError();
-}
-
-int pick_maxnnz(int rpt, int max_row_nnz) {
-  if (max_row_nnz <= 12) return 12;
-  if (max_row_nnz <= 16) return 16;
-  return rpt == 1 ? 32 : 16;  // longer rows take the (rare) global-CSR tail loop
 }
 
 }  // namespace
+
+int resident_slot_width(int M, int max_row_nnz) {
+  const int rpt = (M + kT - 1) / kT;
+  if (max_row_nnz <= 16) return 16;
+  return rpt == 1 ? 32 : 16;  // longer rows take the (rare) CSR tail loop
+}
 
 ResidentGeom resident_geometry(int M, int nnz, int max_row_nnz, int max_row_nnzT, int Fin, int K,
                                int Fout) {
@@ -443,43 +441,42 @@ ResidentGeom resident_geometry(int M, int nnz, int max_row_nnz, int max_row_nnzT
   const int Mp = lds_vertex_stride(M);
   g.rpt = (M + kT - 1) / kT;
   g.nt = (Fout + 31) / 32;
-  g.maxnnz = pick_maxnnz(g.rpt, max_row_nnz);
-  g.maxnnzT = pick_maxnnz(g.rpt, max_row_nnzT);
+  g.maxnnz = resident_slot_width(M, max_row_nnz);
+  g.maxnnzT = resident_slot_width(M, max_row_nnzT);
   const size_t FinK = size_t(Fin) * K;
-  const size_t base = align16(FinK * Fout * 4) + align16(size_t(3) * Fin * Mp * 4);
+  const size_t ring = align16(size_t(Fin) * Mp * 12);
   // The forward always stages the sample's basis in LDS (coalesced store at
   // the end); a shape whose basis block does not fit takes the streaming path.
-  g.fwd_lds = base + size_t(M) * FinK * 4;
+  g.fwd_lds = align16(FinK * Fout * 4) + ring + size_t(M) * FinK * 4;
   g.stage = true;
-  g.bwd_lds = align16(FinK * Mp * 4) + align16(size_t(3) * Fin * Mp * 4) + FinK * Fout * 4;
+  g.bwd_lds = align16(FinK * Mp * 4) + ring + FinK * (Fout + 1) * 4;
   const bool shape_ok = M >= 1 && nnz >= 1 && Fin >= 1 && K >= 1 && Fout >= 1 && g.rpt <= 2;
   // RPT=2 with two Fout tiles spills hundreds of VGPRs: leave it to the streaming path
-  g.fwd_ok = shape_ok && g.nt <= 2 && !(g.rpt == 2 && g.nt == 2) && g.fwd_lds <= size_t(kLdsBytes);
-  g.bwd_ok = shape_ok && g.bwd_lds <= size_t(kLdsBytes);
+  g.fwd_ok = shape_ok && g.nt <= 2 && !(g.rpt == 2 && g.nt == 2) &&
+             !(g.rpt == 2 && g.maxnnz == 32) && g.fwd_lds <= size_t(kLdsBytes);
+  g.bwd_ok = shape_ok && !(g.rpt == 2 && g.maxnnzT == 32) && g.bwd_lds <= size_t(kLdsBytes);
   return g;
 }
 
-hipError_t launch_resident_forward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                   const int* rowptr, const int* col, const float* val,
-                                   const float* x, const float* W, float* basis, float* y,
+hipError_t launch_resident_forward(const ResidentGeom& g, int N, const ResidentFwdArgs& a,
                                    hipStream_t s) {
-#define CG_FWD(R_, Z_, NT_)                                                                  \
-  if (g.rpt == R_ && g.maxnnz == Z_ && g.nt == NT_)                                          \
-    return launch_fwd_t<R_, Z_, NT_>(g, N, M, Fin, K, Fout, rowptr, col, val, x, W, basis, y, \
-                                     s);
-  CG_FWD(1, 12, 1) CG_FWD(1, 16, 1) CG_FWD(1, 32, 1) CG_FWD(2, 12, 1) CG_FWD(2, 16, 1)
-  CG_FWD(1, 12, 2) CG_FWD(1, 16, 2) CG_FWD(1, 32, 2)
+  const bool f1 = a.Fin == 1;
+#define CG_FWD(R_, Z_, NT_)                                 \
+  if (g.rpt == R_ && g.maxnnz == Z_ && g.nt == NT_)         \
+    return f1 ? launch_fwd_t<R_, Z_, NT_, true>(g, N, a, s) \
+              : launch_fwd_t<R_, Z_, NT_, false>(g, N, a, s);
+  CG_FWD(1, 16, 1) CG_FWD(1, 32, 1) CG_FWD(2, 16, 1) CG_FWD(1, 16, 2) CG_FWD(1, 32, 2)
 #undef CG_FWD
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_resident_backward(const ResidentGeom& g, int N, int M, int Fin, int K, int Fout,
-                                    const int* trowptr, const int* tcol, const float* tval,
-                                    const float* dy, const float* W, float* dx, hipStream_t s) {
-#define CG_BWD(R_, Z_)                                                                     \
-  if (g.rpt == R_ && g.maxnnzT == Z_)                                                      \
-    return launch_bwd_t<R_, Z_>(g, N, M, Fin, K, Fout, trowptr, tcol, tval, dy, W, dx, s);
-  CG_BWD(1, 12) CG_BWD(1, 16) CG_BWD(1, 32) CG_BWD(2, 12) CG_BWD(2, 16)
+hipError_t launch_resident_backward(const ResidentGeom& g, int N, const ResidentBwdArgs& a,
+                                    hipStream_t s) {
+  const bool f1 = a.Fin == 1;
+#define CG_BWD(R_, Z_)                  \
+  if (g.rpt == R_ && g.maxnnzT == Z_)   \
+    return f1 ? launch_bwd_t<R_, Z_, true>(g, N, a, s) : launch_bwd_t<R_, Z_, false>(g, N, a, s);
+  CG_BWD(1, 16) CG_BWD(1, 32) CG_BWD(2, 16)
 #undef CG_BWD
   return hipErrorInvalidValue;
 }
