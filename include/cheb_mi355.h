@@ -135,6 +135,32 @@ int cg_adam_update(float* param, const float* grad, float* m, float* v, int64_t 
                    void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Graph coarsening (host code; no device work).
+ * Greedy Graclus matching of one level, lib/coarsening.py:119-165
+ * (metis_one_level): rr/cc/vv are the nnz COO triplets of W in the order
+ * metis() produced them (rows ascending), rid is the visit order of length
+ * n_visit, weights the per-vertex Graclus weights.  The pairing weight
+ * vv * (1/w_i + 1/w_j) is evaluated in the precision of vv/weights (f32: the
+ * NumPy-2 float32 arithmetic of :152; f64 for float64 graphs), first strict
+ * maximum wins.  cluster_id has N = rr[nnz-1] + 1 entries; *n_clusters
+ * receives max(cluster_id) + 1.
+ * ------------------------------------------------------------------------- */
+int cg_graclus_match_f32(int64_t nnz, const int32_t* rr, const int32_t* cc, const float* vv,
+                         int32_t n_visit, const int64_t* rid, const float* weights,
+                         int32_t* cluster_id, int32_t* n_clusters);
+int cg_graclus_match_f64(int64_t nnz, const int32_t* rr, const int32_t* cc, const double* vv,
+                         int32_t n_visit, const int64_t* rid, const double* weights,
+                         int32_t* cluster_id, int32_t* n_clusters);
+/* Binary-tree vertex order of lib/coarsening.py:167-214 (compute_perm).
+ * parents: `levels` arrays concatenated, level l has sizes[l] entries
+ * (sizes[levels] = number of coarsest vertices = max(parents[levels-1]) + 1).
+ * perm_out receives the orders of level 0..levels concatenated; the order of
+ * level l has sizes_out[l] = n_coarsest * 2^(levels-l) entries.  perm_cap is
+ * the capacity of perm_out in entries (>= n_coarsest * (2^(levels+1) - 1)). */
+int cg_compute_perm(int32_t levels, const int32_t* sizes, const int32_t* parents,
+                    int32_t* perm_out, int64_t perm_cap, int32_t* sizes_out);
+
+/* ---------------------------------------------------------------------------
  * Data-parallel gradient exchange over RCCL (xGMI), for callers that do not
  * use torch.distributed.  One communicator per process/GPU; the unique id is
  * created on rank 0 and shipped by the caller (file, socket, store).
