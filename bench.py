@@ -5,11 +5,21 @@ Workload (BASELINE.json configs[1]): MNIST 8-NN grid
 graph coarsened to M=976 vertices (nnz(L~)=6396), K=25, Fin=1, Fout=32,
 batch 256 per GPU, fp32.  One step = one training step of the chebyshev5
 filter on synthetic data already resident in HBM:
-    forward  (basis + y = basis W)          -> cg_cheb_forward
-    backward (dx, dW) with a fixed N(0,1) upstream gradient dy -> cg_cheb_backward
+    forward  (basis + y = basis W)                     -> cg_cheb_forward
+    backward (dx, dW) with a fixed N(0,1) upstream dy   -> cg_cheb_backward
     all-reduce(sum) of dW over ranks (RCCL), N>1 only
-    Adam update of W (TF-1.x rule, grad scaled by 1/world)   -> cg_adam_update
-Weak scaling: every rank processes its own batch of 256.
+    Adam update of W (TF-1.x rule, grad scaled by 1/world) -> cg_adam_update
+Weak scaling: every rank processes its own batch of 256 (the batch dimension
+is sharded; L~ and W are replicated -- SURVEY.md §8e).
+
+The timed loop issues exactly those C-ABI calls on torch's current stream
+(ctypes, pre-bound arguments, no per-step allocation or event), bracketed by
+barrier + synchronize; the max over ranks is reported.  After it, each kernel
+is timed alone in bursts of back-to-back launches with HIP events recorded on
+the same stream (roofline.achieved); rocprofv3 summaries of the same command
+live under profiles/ (scripts/prof_pmc.sh), whose PMC-measured HBM bytes of
+the dominant kernel are reported as roofline.traffic when they match this
+configuration.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
         (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -18,6 +28,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -31,13 +42,15 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from cnn_graph_amd import _lib  # noqa: E402
 from cnn_graph_amd import dist as cdist  # noqa: E402
 from cnn_graph_amd import ops  # noqa: E402
 from cnn_graph_amd.graph_conv import truncated_normal_  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-MFMA_F32_PEAK_TF = 157.3   # dense fp32 MFMA
+MFMA_F32_PEAK_TF = 157.3   # dense fp32 MFMA (= fp32 vector peak)
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
 def load_config_b():
@@ -50,7 +63,8 @@ def load_config_b():
 
 
 def algorithmic_bytes(M, nnz, B, K):
-    """SURVEY.md §8d per-launch algorithmic bytes of the K-step SpMM basis."""
+    """SURVEY.md §8d per-launch algorithmic bytes of the K-step SpMM basis
+    (forward) and of the reverse recurrence (backward); B = Fin * N_local."""
     csr = 8 * nnz + 4 * (M + 1)
     fwd = (K - 1) * csr + 4 * M * B * (2 + 3 * (K - 2))
     bwd = (K - 1) * csr + 4 * M * B * (3 + 5 * (K - 2))
@@ -83,7 +97,41 @@ def cpu_baseline(L, fake, K, Fout, seconds=12.0, threads=16):
                 break
     return {"value": round(reps * n / el, 1), "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": f"{reps} fwd+bwd passes of a 32-sample batch of config B (oracle/cheb_oracle.py, "
-                      f"fp32, scipy SpMM + numpy BLAS, {threads} BLAS threads), {el:.1f}s"}
+                      f"fp32, scipy SpMM single-threaded + numpy BLAS with {threads} threads), {el:.1f}s; "
+                      f"host has {os.cpu_count()} logical CPUs"}
+
+
+def burst_ms(fn, reps=50, rounds=5):
+    """Median over rounds of the mean per-launch time of `reps` back-to-back
+    launches, HIP events recorded on torch's current stream (the launch stream)."""
+    vals = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        vals.append(e0.elapsed_time(e1) / reps)
+    return float(np.median(vals))
+
+
+def pmc_traffic(kernel, cfg):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (scripts/prof_pmc.sh -> profiles/pmc_latest.json) if it was taken on this
+    configuration: FETCH_SIZE x 2 (gfx950 correction for wide coalesced reads,
+    MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both KB -> bytes."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("config") != cfg:
+        return None, None
+    c = d.get("counters", {}).get(kernel)
+    if not c or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+        return None, None
+    return int(c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024), d.get("source")
 
 
 def main():
@@ -119,33 +167,31 @@ def main():
     v_adam = torch.zeros_like(W)
 
     runner = ops.ChebRunner(plan, N, Fin, K, Fout, dev)
-    ev = {k: [] for k in ("fwd", "bwd")}
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    adam = _lib.lib().cg_adam_update
+    adam_args = (W.data_ptr(), runner.dW.data_ptr(), m_adam.data_ptr(), v_adam.data_ptr(),
+                 W.numel(), ctypes.c_float(1e-3), ctypes.c_float(0.9), ctypes.c_float(0.999),
+                 ctypes.c_float(1e-8))
+    scale = ctypes.c_float(1.0 / world)
 
-    def step(i, timed):
-        if timed:
-            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e0.record()
-        runner.forward(x, W)
-        if timed:
-            e1.record()
-        _dx, dW = runner.backward(dy, W)
-        if timed:
-            e2.record()
-            ev["fwd"].append((e0, e1))
-            ev["bwd"].append((e1, e2))
+    def step(i):
+        runner.forward(x, W, stream=stream)
+        runner.backward(dy, W, stream=stream)
         if world > 1:
-            dist.all_reduce(dW, op=dist.ReduceOp.SUM)
-        ops.adam_update(W, dW, m_adam, v_adam, i + 1, lr=1e-3, grad_scale=1.0 / world)
+            dist.all_reduce(runner.dW, op=dist.ReduceOp.SUM)
+        st = adam(*adam_args, i + 1, scale, stream)
+        if st:
+            _lib.check("cg_adam_update", st)
 
     for i in range(args.warmup):
-        step(i, False)
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, True)
+        step(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -156,17 +202,24 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["fwd"]]))
-    bwd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["bwd"]]))
+    # per-kernel timing (after the timed region): forward = one kernel;
+    # backward = the recurrence kernel + the tiny fixed-order dW slab reduce
+    fwd_ms = burst_ms(lambda: runner.forward(x, W, stream=stream))
+    bwd_ms = burst_ms(lambda: runner.backward(dy, W, stream=stream))
     B = N * Fin
     bytes_fwd, bytes_bwd, _csr = algorithmic_bytes(M, plan.nnz, B, K)
     compulsory_fwd = 4 * (N * M * Fin + N * M * Fin * K + N * M * Fout) + 8 * plan.nnz + 4 * (M + 1)
+    fwd_kernel = "cheb_fwd_fast" if path == "resident" else "stream_fwd"
+    bwd_kernel = "cheb_bwd_fast" if path == "resident" else "stream_bwd"
     kern = {
-        "fwd": {"ms": fwd_ms, "alg_bytes": bytes_fwd},
-        "bwd": {"ms": bwd_ms, "alg_bytes": bytes_bwd},
+        "fwd": {"kernel": fwd_kernel, "ms": fwd_ms, "alg_bytes": bytes_fwd},
+        "bwd": {"kernel": bwd_kernel + "+k_reduce_slabs", "ms": bwd_ms, "alg_bytes": bytes_bwd},
     }
     dom = max(kern, key=lambda k: kern[k]["ms"])
     ach = kern[dom]["alg_bytes"] / (kern[dom]["ms"] * 1e-3) / 1e9
+    cfg_key = {"M": M, "N": N, "K": K, "Fin": Fin, "Fout": Fout}
+    traffic, traffic_src = pmc_traffic(kern[dom]["kernel"].split("+")[0], cfg_key)
+    contraction_tflops = 2.0 * N * M * Fin * K * Fout / (fwd_ms * 1e-3) / 1e12
 
     value = N * world * args.steps / elapsed
     out = {
@@ -187,15 +240,20 @@ def main():
                                "Fout=32, chebyshev5 fwd+bwd + dW all-reduce + Adam",
                    "batch_per_gpu": N, "global_batch": N * world, "M": M, "nnz": plan.nnz, "K": K,
                    "Fin": Fin, "Fout": Fout, "path": path, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": "cheb_fwd_resident" if dom == "fwd" and path == "resident"
-                     else ("cheb_bwd_resident" if path == "resident" else f"stream_{dom}"),
+        "roofline": {"bound": "hbm", "kernel": kern[dom]["kernel"],
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
                      "alg_bytes_per_launch": kern[dom]["alg_bytes"],
-                     "avg_launch_ms": round(kern[dom]["ms"], 5)},
-        "kernels": {k: {"avg_ms": round(v["ms"], 5), "alg_bytes": v["alg_bytes"],
+                     "avg_launch_ms": round(kern[dom]["ms"], 5),
+                     "timing": "HIP events on the launch stream around 50 back-to-back launches",
+                     "traffic_source": traffic_src},
+        "kernels": {k: {"kernel": v["kernel"], "avg_ms": round(v["ms"], 5), "alg_bytes": v["alg_bytes"],
                         "alg_GBps": round(v["alg_bytes"] / (v["ms"] * 1e-3) / 1e9, 1)}
                     for k, v in kern.items()},
+        "contraction_mfma": {"tflops_over_fwd_kernel": round(contraction_tflops, 2),
+                             "peak_tflops": MFMA_F32_PEAK_TF,
+                             "frac": round(contraction_tflops / MFMA_F32_PEAK_TF, 4)},
         "compulsory_fwd_bytes": compulsory_fwd,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

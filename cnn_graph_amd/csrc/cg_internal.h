@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 namespace cg {
 
@@ -81,6 +82,66 @@ hipError_t launch_resident_forward(const ResidentGeom& g, int N, const ResidentF
                                    hipStream_t s);
 hipError_t launch_resident_backward(const ResidentGeom& g, int N, const ResidentBwdArgs& a,
                                     hipStream_t s);
+
+// ---- fast resident path (cheb_fast.hip): M <= 1024, rows <= 16 nnz, Fin in {1,2,4}
+constexpr int kFastWidth = 16;  // register slots per row
+// Device image of a sparse operand for the fast kernels (built on the host by
+// cheb_abi.cpp::build_fast_image).  Thread t owns row[t] (-1 = idle); its
+// own ring record is rpos[t] and its CSR entries gather records cpos[j][t]
+// (j < 16, column-major; padding gathers the zero record zpos with val 0).
+// mpos[m] is the record of vertex m (m < 32*ceil(M/32); zpos past M);
+// wlen[w] the max row length of wave w.  Records: P (>= M + 2, incl. the zero
+// record and a dummy record that idle lanes write).
+struct FastImage {
+  const int* row;
+  const int* rpos;   // own record, copy 0 (written every step)
+  const int* rpos1;  // own record, copy 1 (written every step)
+  const int* rposr;  // own record copy read as T_{k-2}
+  const int* cpos;
+  const float* val;
+  const int* wlen;
+  const int* mpos;
+  const int* pos0;   // [M] copy-0 record of vertex m (T_0 initialisation)
+  const int* pos1;   // [M] copy-1 record of vertex m
+  int zpos;          // first of the 32 zero records (positions zpos .. zpos+31)
+  int P;
+};
+// Host-side layout plan (lds_layout.cpp): thread->row assignment, two bank-
+// aware record copies per vertex, per-gather copy choice.
+struct FastLayout {
+  std::vector<int> row, wlen, cpos, rpos0, rpos1, rposr, mpos, pos0, pos1;
+  int P = 0, zero_base = 0, dummy_base = 0;
+  long gather_cycles = 0, gather_ideal = 0;  // modelled LDS cycles of one step's gathers
+};
+void plan_fast_layout(int M, const int32_t* rp, const int32_t* ci, FastLayout* out);
+struct FastGeom {
+  int nt;            // 32-wide Fout tiles (forward)
+  bool dw_fused;     // backward computes the dW partial in-kernel (FinK, Fout <= 32)
+  size_t dscratch;   // bytes of the backward's dBasis / dW-reduce LDS region
+  size_t fwd_lds, bwd_lds;
+  bool fwd_ok, bwd_ok;
+};
+FastGeom fast_geometry(int M, int P, int max_row_nnz, int max_row_nnzT, int Fin, int K, int Fout);
+struct FastFwdArgs {
+  int M, Fin, K, Fout, dbg;
+  FastImage E;  // L~
+  const float* x;
+  const float* W;
+  float* basis;
+  float* y;
+};
+struct FastBwdArgs {
+  int M, Fin, K, Fout, Mp, dbg;
+  size_t dscratch_bytes;
+  FastImage E;  // L~^T
+  const float* dy;
+  const float* basis;  // read by the fused dW
+  const float* W;
+  float* dx;
+  float* dw_slab;      // [N][FinK][Fout] per-sample dW partials, or NULL (no fused dW)
+};
+hipError_t launch_fast_forward(const FastGeom& g, int N, const FastFwdArgs& a, hipStream_t s);
+hipError_t launch_fast_backward(const FastGeom& g, int N, const FastBwdArgs& a, hipStream_t s);
 
 // ---- streaming path ----------------------------------------------------------
 hipError_t launch_x_to_cols(const float* x, float* T0, float* basis, int N, int M, int Fin, int K,

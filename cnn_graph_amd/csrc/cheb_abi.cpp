@@ -38,6 +38,13 @@ struct cg_plan {
     int* buf = nullptr;  // one allocation: row | len | beg | col | val | wlen
     cg::SlotLayout view{};
   } slots, tslots;
+  // images of L~ and L~^T for the fast resident kernels (cheb_fast.hip)
+  struct Fast {
+    void* buf = nullptr;
+    cg::FastImage view{};
+    bool ok = false;  // max row length <= cg::kFastWidth and M <= 1024
+    long gather_cycles = 0, gather_ideal = 0;  // modelled LDS cycles per step
+  } fast, tfast;
 };
 
 namespace {
@@ -173,6 +180,59 @@ int build_slots(cg_plan::Slots* out, int32_t M, const int32_t* rp, const int32_t
   return CG_OK;
 }
 
+// Image of a CSR operand for the fast resident kernels (cg_internal.h::
+// FastImage): thread->row assignment and bank-aware record layout from
+// lds_layout.cpp, uploaded as one device allocation.
+int build_fast_image(cg_plan::Fast* out, int32_t M, const int32_t* rp, const int32_t* ci,
+                     const float* v) {
+  constexpr int kT = 1024, kWd = cg::kFastWidth;
+  if (M > kT) return CG_OK;
+  int maxlen = 0;
+  for (int32_t r = 0; r < M; ++r) maxlen = std::max(maxlen, rp[r + 1] - rp[r]);
+  if (maxlen > kWd) return CG_OK;
+  cg::FastLayout lay;
+  cg::plan_fast_layout(M, rp, ci, &lay);
+  std::vector<float> val(size_t(kWd) * kT, 0.f);
+  for (int t = 0; t < kT; ++t) {
+    const int r = lay.row[size_t(t)];
+    if (r < 0) continue;
+    for (int j = 0; j < rp[r + 1] - rp[r]; ++j) val[size_t(j) * kT + t] = v[rp[r] + j];
+  }
+  const std::vector<int>* ints[] = {&lay.row, &lay.rpos0, &lay.rpos1, &lay.rposr, &lay.cpos,
+                                    &lay.wlen, &lay.mpos, &lay.pos0, &lay.pos1};
+  size_t bytes = val.size() * 4;
+  for (const auto* a : ints) bytes += a->size() * 4;
+  char* d = nullptr;
+  CG_HIP(hipMalloc(reinterpret_cast<void**>(&d), bytes));
+  out->buf = d;
+  size_t o = 0;
+  bool okc = true;
+  auto put = [&](const void* src, size_t count) -> const void* {
+    const void* at = d + o;
+    if (hipMemcpy(d + o, src, count * 4, hipMemcpyHostToDevice) != hipSuccess) okc = false;
+    o += count * 4;
+    return at;
+  };
+  cg::FastImage& e = out->view;
+  e.row = static_cast<const int*>(put(lay.row.data(), lay.row.size()));
+  e.rpos = static_cast<const int*>(put(lay.rpos0.data(), lay.rpos0.size()));
+  e.rpos1 = static_cast<const int*>(put(lay.rpos1.data(), lay.rpos1.size()));
+  e.rposr = static_cast<const int*>(put(lay.rposr.data(), lay.rposr.size()));
+  e.cpos = static_cast<const int*>(put(lay.cpos.data(), lay.cpos.size()));
+  e.val = static_cast<const float*>(put(val.data(), val.size()));
+  e.wlen = static_cast<const int*>(put(lay.wlen.data(), lay.wlen.size()));
+  e.mpos = static_cast<const int*>(put(lay.mpos.data(), lay.mpos.size()));
+  e.pos0 = static_cast<const int*>(put(lay.pos0.data(), lay.pos0.size()));
+  e.pos1 = static_cast<const int*>(put(lay.pos1.data(), lay.pos1.size()));
+  e.zpos = lay.zero_base;
+  e.P = lay.P;
+  if (!okc) return fail(CG_ERR_HIP, "build_fast_image: hipMemcpy failed");
+  out->gather_cycles = lay.gather_cycles;
+  out->gather_ideal = lay.gather_ideal;
+  out->ok = true;
+  return CG_OK;
+}
+
 template <typename T>
 int upload(T** dst, const T* src, size_t count) {
   *dst = nullptr;
@@ -189,6 +249,8 @@ void free_plan(cg_plan* p) {
     if (q) (void)hipFree(q);
   if (p->slots.buf) (void)hipFree(p->slots.buf);
   if (p->tslots.buf) (void)hipFree(p->tslots.buf);
+  if (p->fast.buf) (void)hipFree(p->fast.buf);
+  if (p->tfast.buf) (void)hipFree(p->tfast.buf);
   if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
   if (p->ev_join) (void)hipEventDestroy(p->ev_join);
   if (p->side) (void)hipStreamDestroy(p->side);
@@ -213,10 +275,28 @@ int check_shape(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fou
   return CG_OK;
 }
 
+// Debug bit 24 forces the classic resident kernels (cheb_resident.hip) where
+// the fast ones (cheb_fast.hip) would run; bit 25 disables the fused dW.
+cg::FastGeom fast_geom(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout) {
+  return cg::fast_geometry(p->M, p->fast.view.P, p->max_row_nnz, p->max_row_nnzT, Fin, K, Fout);
+}
+
+bool use_fast(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool backward) {
+  if (cg::g_debug_flags & (1 << 24)) return false;
+  if (!(backward ? p->tfast.ok : p->fast.ok)) return false;
+  const cg::FastGeom g = fast_geom(p, Fin, K, Fout);
+  return backward ? g.bwd_ok : g.fwd_ok;
+}
+
+bool fused_dw(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout) {
+  return use_fast(p, Fin, K, Fout, true) && fast_geom(p, Fin, K, Fout).dw_fused &&
+         !(cg::g_debug_flags & (1 << 25));
+}
+
 int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool backward,
                 int* path) {
   const cg::ResidentGeom g = cg::resident_geometry(p->M, int(p->nnz), p->max_row_nnz, p->max_row_nnzT, Fin, K, Fout);
-  const bool fits = backward ? g.bwd_ok : g.fwd_ok;
+  const bool fits = use_fast(p, Fin, K, Fout, backward) || (backward ? g.bwd_ok : g.fwd_ok);
   if (p->path == CG_PATH_STREAM) {
     *path = CG_PATH_STREAM;
   } else if (p->path == CG_PATH_RESIDENT) {
@@ -250,8 +330,11 @@ StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t 
   return w;
 }
 
-size_t dw_slab_bytes(int64_t R, int FinK, int Fout) {
-  return al256(size_t(cg::dw_chunks(R)) * size_t(FinK) * size_t(Fout) * 4);
+// dW partial slabs: dw_chunks(R) of them from k_dw_slabs, or one per sample
+// from the fused backward.
+size_t dw_slab_bytes(int64_t R, int32_t N, int FinK, int Fout) {
+  const size_t n = std::max<size_t>(size_t(cg::dw_chunks(R)), size_t(N));
+  return al256(n * size_t(FinK) * size_t(Fout) * 4);
 }
 
 // Workspace layout.  forward: [T ring] (streaming path only).
@@ -262,7 +345,7 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
   if ((rc = choose_path(p, Fin, K, Fout, false, &pf))) return rc;
   if ((rc = choose_path(p, Fin, K, Fout, true, &pb))) return rc;
   const StreamWs w = stream_ws(p, N, Fin, K, Fout);
-  const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, Fin * K, Fout);
+  const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, N, Fin * K, Fout);
   *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.ring;
   *bwd = slabs + ((pb == CG_PATH_RESIDENT) ? 0 : (w.ring + w.dA));
   return CG_OK;
@@ -297,6 +380,51 @@ int cg_internal_set_error(int code, const char* msg) {
 }
 
 const char* cg_last_error(void) { return g_err.c_str(); }
+
+// Not in the public header (tests / diagnostics): plan the fast-path LDS layout
+// of a host CSR operand without a GPU, check its invariants, and report the
+// modelled LDS cycles of one step's gathers (with the layout and conflict-free).
+int cg_debug_layout_stats(int32_t M, const int32_t* rowptr, const int32_t* col,
+                          long* gather_cycles, long* gather_ideal, int* records) {
+  if (M < 1 || M > 1024 || !rowptr || !col) return fail(CG_ERR_ARG, "layout_stats: bad args");
+  for (int r = 0; r < M; ++r)
+    if (rowptr[r + 1] - rowptr[r] > cg::kFastWidth)
+      return fail(CG_ERR_UNSUPPORTED, "layout_stats: row %d longer than %d", r, cg::kFastWidth);
+  cg::FastLayout lay;
+  cg::plan_fast_layout(M, rowptr, col, &lay);
+  std::vector<int> seen(size_t(lay.P), 0);
+  for (int v = 0; v < M; ++v) {
+    for (int p : {lay.pos0[size_t(v)], lay.pos1[size_t(v)]}) {
+      if (p < 64 || p >= lay.P || seen[size_t(p)]++)
+        return fail(CG_ERR_ARG, "layout: bad/duplicate record %d of vertex %d", p, v);
+    }
+  }
+  for (int t = 0; t < 1024; ++t) {
+    const int r = lay.row[size_t(t)];
+    for (int j = 0; j < cg::kFastWidth; ++j) {
+      const int p = lay.cpos[size_t(j) * 1024 + t];
+      if (r >= 0 && j < rowptr[r + 1] - rowptr[r]) {
+        const int c = col[rowptr[r] + j];
+        if (p != lay.pos0[size_t(c)] && p != lay.pos1[size_t(c)])
+          return fail(CG_ERR_ARG, "layout: thread %d slot %d reads record %d, not vertex %d", t, j, p, c);
+      } else if (p >= 32) {
+        return fail(CG_ERR_ARG, "layout: padding of thread %d slot %d is not a zero record", t, j);
+      }
+    }
+    if (r >= 0 && (lay.rpos0[size_t(t)] != lay.pos0[size_t(r)] || lay.rpos1[size_t(t)] != lay.pos1[size_t(r)] ||
+                   (lay.rposr[size_t(t)] != lay.pos0[size_t(r)] && lay.rposr[size_t(t)] != lay.pos1[size_t(r)])))
+      return fail(CG_ERR_ARG, "layout: own records of thread %d", t);
+    if (r < 0 && (lay.rpos0[size_t(t)] < 32 || lay.rpos0[size_t(t)] >= 64))
+      return fail(CG_ERR_ARG, "layout: idle thread %d does not write a dummy record", t);
+  }
+  for (int m = 0; m < M; ++m)
+    if (lay.mpos[size_t(m)] != lay.pos0[size_t(m)] && lay.mpos[size_t(m)] != lay.pos1[size_t(m)])
+      return fail(CG_ERR_ARG, "layout: tile read of vertex %d", m);
+  if (gather_cycles) *gather_cycles = lay.gather_cycles;
+  if (gather_ideal) *gather_ideal = lay.gather_ideal;
+  if (records) *records = lay.P;
+  return ok();
+}
 
 int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz, const int32_t* rowptr,
                    const int32_t* col, const float* val, const int32_t* t_rowptr,
@@ -342,6 +470,8 @@ int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz, const int
   if (!rc) rc = upload(&p->tval, tv.data(), tv.size());
   if (!rc && nnz > 0) rc = build_slots(&p->slots, M, rowptr, col, val);
   if (!rc && nnz > 0) rc = build_slots(&p->tslots, M, trp.data(), tci.data(), tv.data());
+  if (!rc && nnz > 0) rc = build_fast_image(&p->fast, M, rowptr, col, val);
+  if (!rc && nnz > 0) rc = build_fast_image(&p->tfast, M, trp.data(), tci.data(), tv.data());
   (void)hipSetDevice(prev);
   if (rc) {
     free_plan(p);
@@ -398,6 +528,21 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int M = plan->M;
 
+  if (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, false)) {
+    cg::FastFwdArgs a{};
+    a.M = M;
+    a.Fin = Fin;
+    a.K = K;
+    a.Fout = Fout;
+    a.dbg = cg::g_debug_flags & 0xff;
+    a.E = plan->fast.view;
+    a.x = x;
+    a.W = y ? W : nullptr;
+    a.basis = basis;
+    a.y = y;
+    CG_HIP(cg::launch_fast_forward(fast_geom(plan, Fin, K, Fout), N, a, s));
+    return ok();
+  }
   if (path == CG_PATH_RESIDENT) {
     const cg::ResidentGeom g = cg::resident_geometry(M, int(plan->nnz), plan->max_row_nnz, plan->max_row_nnzT, Fin, K, Fout);
     cg::ResidentFwdArgs a{};
@@ -461,7 +606,7 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
   if ((rc = ensure_side_stream(plan))) return rc;
   char* base = static_cast<char*>(workspace);
   float* slabs = reinterpret_cast<float*>(base);
-  char* rest = base + dw_slab_bytes(R, FinK, Fout);
+  char* rest = base + dw_slab_bytes(R, N, FinK, Fout);
   // Measured on MI355X: a hipEventRecord/hipStreamWaitEvent fork+join costs
   // ~20 us per call, far more than the overlap gains, so it is opt-in
   // (cg_debug_set_flags bit 21) and dW normally runs on the caller's stream.
@@ -471,8 +616,26 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
     CG_HIP(hipEventRecord(plan->ev_fork, s));
     CG_HIP(hipStreamWaitEvent(plan->side, plan->ev_fork, 0));
   }
+  const bool fused = dx != nullptr && path == CG_PATH_RESIDENT && fused_dw(plan, Fin, K, Fout);
   if (dx) {
-    if (path == CG_PATH_RESIDENT) {
+    if (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, true)) {
+      const cg::FastGeom g = fast_geom(plan, Fin, K, Fout);
+      cg::FastBwdArgs a{};
+      a.M = M;
+      a.Fin = Fin;
+      a.K = K;
+      a.Fout = Fout;
+      a.Mp = cg::lds_vertex_stride(M);
+      a.dbg = (cg::g_debug_flags >> 8) & 0xff;
+      a.dscratch_bytes = g.dscratch;
+      a.E = plan->tfast.view;
+      a.dy = dy;
+      a.basis = basis;
+      a.W = W;
+      a.dx = dx;
+      a.dw_slab = fused ? slabs : nullptr;
+      CG_HIP(cg::launch_fast_backward(g, N, a, s));
+    } else if (path == CG_PATH_RESIDENT) {
       const cg::ResidentGeom g = cg::resident_geometry(M, int(plan->nnz), plan->max_row_nnz,
                                                        plan->max_row_nnzT, Fin, K, Fout);
       cg::ResidentBwdArgs a{};
@@ -503,14 +666,14 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
                                         G(k), dA, dx, N, M, Fin, K, k, s));
     }
   }
-  if (!(cg::g_debug_flags & (1 << 22)))  // ablation hook: skip dW
+  if (!fused && !(cg::g_debug_flags & (1 << 22)))  // ablation hook: skip dW
     CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, sdw));
   if (overlap) {
     CG_HIP(hipEventRecord(plan->ev_join, plan->side));
     CG_HIP(hipStreamWaitEvent(s, plan->ev_join, 0));
   }
   if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
-    CG_HIP(cg::launch_reduce_slabs(slabs, chunks, int64_t(FinK) * Fout, dW, s));
+    CG_HIP(cg::launch_reduce_slabs(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, s));
   return ok();
 }
 

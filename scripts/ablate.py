@@ -18,12 +18,12 @@ import bench  # noqa: E402
 from cnn_graph_amd import _lib, ops  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
-FWD = {"full": 0, "no_spmm": 1, "no_basis_store": 2, "no_mfma": 4, "no_y_store": 8,
-       "no_stores": 2 | 8, "only_spmm": 2 | 4 | 8, "nothing": 1 | 2 | 4 | 8, "prologue": 16}
-BWD = {"full": 0, "no_phaseA": 1, "no_clenshaw_spmm": 2, "no_dw": 1 << 14,
-       "only_dw": 16 | (1 << 15), "only_A": 2 | (1 << 14), "only_B": 1 | (1 << 14),
-       "no_reduce": 1 << 15, "prologue": 16 | (1 << 14) | (1 << 15),
-       "nothing": 1 | 2 | (1 << 14) | (1 << 15)}
+# raw cg_debug_set_flags values: bits 0-7 forward kernel, 8-15 backward kernel,
+# 22 skip dW, 23 skip slab reduce, 24 classic resident kernels, 25 no fused dW
+FWD = {"full": 0, "no_basis_store": 2, "no_mfma": 4, "no_y_store": 8, "no_stores": 2 | 8,
+       "only_spmm": 2 | 4 | 8, "prologue": 16, "classic": 1 << 24}
+BWD = {"full": 0, "no_phaseA": 2 << 8, "prologue": 16 << 8, "no_fused_dw": 1 << 25,
+       "no_dw": (1 << 25) | (1 << 22), "no_reduce": 1 << 23, "classic": 1 << 24}
 
 
 def main():
@@ -71,7 +71,7 @@ def main():
             h.cg_debug_set_flags(f)
             res[f"fwd:{k}"].append(t_fwd())
         for k, f in BWD.items():
-            h.cg_debug_set_flags(f << 8)
+            h.cg_debug_set_flags(f)
             res[f"bwd:{k}"].append(t_bwd())
     h.cg_debug_set_flags(0)
     out = {k: round(float(np.median(v)), 2) for k, v in res.items()}
@@ -80,8 +80,8 @@ def main():
     for Kx in (2, 7, 13, 25):
         Wx = torch.randn((Kx, Fout), device=dev) * 0.1
         rx = ops.ChebRunner(plan, N, Fin, Kx, Fout, dev)
-        for name, f in (("fwd_full", 0), ("fwd_nothing", FWD["nothing"]), ("bwd_full", 0),
-                        ("bwd_nothing", BWD["nothing"])):
+        for name, f in (("fwd_full", 0), ("fwd_only_spmm", FWD["only_spmm"]), ("bwd_full", 0),
+                        ("bwd_no_dw", BWD["no_dw"])):
             vals = []
             for _ in range(args.rounds):
                 if name.startswith("fwd"):
@@ -92,7 +92,7 @@ def main():
                         rx.forward(x, Wx)
                     e1.record()
                 else:
-                    h.cg_debug_set_flags(f << 8)
+                    h.cg_debug_set_flags(f)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                     for _ in range(args.reps):

@@ -19,8 +19,11 @@ def short(name):
     return m.group(1) if m else name[:40]
 
 
-def main(root):
-    out = {"kernels": {}, "counters": {}}
+def main(root, tag=None):
+    # the bench configuration these passes ran (bench.py defaults: config B)
+    out = {"config": {"M": 976, "N": 256, "K": 25, "Fin": 1, "Fout": 32},
+           "source": f"rocprofv3 passes of `bench.py --steps 50 --warmup 10` ({tag or root})",
+           "kernels": {}, "counters": {}}
     for f in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
@@ -51,4 +54,4 @@ def main(root):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out", sys.argv[2] if len(sys.argv) > 2 else None)

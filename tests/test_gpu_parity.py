@@ -26,6 +26,23 @@ def dev(built_lib):
     return torch.device("cuda", 0)
 
 
+# Kernel variants of the resident path (debug bits of cg_debug_set_flags):
+# "fast" = cheb_fast.hip with the fused dW (default), "fast_nofuse" = fast
+# kernels + the separate dW GEMM, "classic" = cheb_resident.hip.
+VARIANTS = {"fast": 0, "fast_nofuse": 1 << 25, "classic": 1 << 24}
+
+
+@pytest.fixture(params=list(VARIANTS))
+def variant(request, dev):
+    import ctypes
+    from cnn_graph_amd import _lib
+    h = _lib.lib()
+    h.cg_debug_set_flags.argtypes = [ctypes.c_int]
+    h.cg_debug_set_flags(VARIANTS[request.param])
+    yield request.param
+    h.cg_debug_set_flags(0)
+
+
 def make_plan(c, path):
     from cnn_graph_amd.plan import ChebPlan
     M = c["M"]
@@ -42,6 +59,34 @@ def test_native_library_is_the_in_tree_build(dev):
     assert os.path.dirname(_lib.LIB_PATH).endswith("cnn_graph_amd")
     with open("/proc/self/maps") as f:
         assert any("libcheb_mi355.so" in line for line in f)
+
+
+@pytest.mark.parametrize("fname,prefix", CASES, ids=CASE_IDS)
+def test_resident_variants_golden(dev, variant, fname, prefix):
+    test_forward_backward_golden(dev, fname, prefix, "resident")
+
+
+@pytest.mark.parametrize("fin", [1, 2, 4])
+def test_fast_path_fin_widths_vs_oracle(dev, variant, fin):
+    """Fin in {1, 2, 4} (record-vector gathers) on the MNIST graph vs the oracle."""
+    from cnn_graph_amd import ops
+    g = load_golden("golden_B.npz")
+    c = case(g)
+    rng = np.random.default_rng(7 + fin)
+    N, K, Fout = 6, 7, 24
+    x = rng.random((N, c["M"], fin), dtype=np.float32)
+    W = (rng.standard_normal((fin * K, Fout)) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((N, c["M"], Fout)).astype(np.float32)
+    plan = make_plan(c, "resident")
+    basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), K)
+    dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), K)
+    torch.cuda.synchronize()
+    ob, oy = O.cheb_forward(x, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], W, K)
+    assert np.array_equal(basis.cpu().numpy(), ob)
+    assert O.normwise_err(y.cpu().numpy(), oy) < TOL
+    odx, odW = O.cheb_backward(dy, ob, W, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], N, c["M"], fin, K)
+    assert O.normwise_err(dx.cpu().numpy(), odx) < TOL
+    assert O.normwise_err(dW.cpu().numpy(), odW) < TOL
 
 
 @pytest.mark.parametrize("path", ["resident", "stream"])
@@ -62,7 +107,7 @@ def test_forward_backward_golden(dev, fname, prefix, path):
     assert O.normwise_err(dW.cpu().numpy(), c["dW_ref"]) < TOL
 
 
-@pytest.mark.parametrize("path", ["resident", "stream"])
+@pytest.mark.parametrize("path", ["resident", "stream", "classic"])
 def test_config_b_full_batch_vs_oracle(dev, path):
     """BASELINE config B at full size (N=256, M=976, K=25, Fout=32)."""
     from cnn_graph_amd import ops
@@ -74,10 +119,18 @@ def test_config_b_full_batch_vs_oracle(dev, path):
     x[:, g["fake_rows"], :] = 0
     W = c["W"]
     dy = rng.standard_normal((N, c["M"], c["Fout"])).astype(np.float32)
-    plan = make_plan(c, path)
-    basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), c["K"])
-    dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), c["K"])
-    torch.cuda.synchronize()
+    import ctypes
+    from cnn_graph_amd import _lib
+    h = _lib.lib()
+    h.cg_debug_set_flags.argtypes = [ctypes.c_int]
+    h.cg_debug_set_flags(VARIANTS["classic"] if path == "classic" else 0)
+    try:
+        plan = make_plan(c, "resident" if path == "classic" else path)
+        basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), c["K"])
+        dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), c["K"])
+        torch.cuda.synchronize()
+    finally:
+        h.cg_debug_set_flags(0)
     ob, oy = O.cheb_forward(x, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], W, c["K"])
     assert np.array_equal(basis.cpu().numpy(), ob)
     assert O.normwise_err(y.cpu().numpy(), oy) < TOL
