@@ -6,19 +6,24 @@ SRC_DIR  := cnn_graph_amd/csrc
 OBJ_DIR  ?= build/obj
 LIB      ?= cnn_graph_amd/libcheb_mi355.so
 SRCS     := $(SRC_DIR)/cheb_fast.hip $(SRC_DIR)/cheb_resident.hip $(SRC_DIR)/cheb_stream.hip $(SRC_DIR)/graph_ops.hip \
+            $(SRC_DIR)/lstm.hip \
             $(SRC_DIR)/cheb_abi.cpp $(SRC_DIR)/comm.cpp $(SRC_DIR)/coarsen.cpp \
             $(SRC_DIR)/lds_layout.cpp
 OBJS     := $(patsubst $(SRC_DIR)/%,$(OBJ_DIR)/%.o,$(SRCS))
-HDRS     := $(SRC_DIR)/cg_internal.h include/cheb_mi355.h
+DEPS     := $(OBJS:.o=.d)
 
 all: $(LIB)
 
-$(OBJ_DIR)/%.o: $(SRC_DIR)/% $(HDRS)
+# header dependencies are tracked per object (-MMD), so touching the public
+# header does not rebuild the (slow) resident-kernel translation units
+$(OBJ_DIR)/%.o: $(SRC_DIR)/%
 	@mkdir -p $(OBJ_DIR)
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+	$(HIPCC) $(CXXFLAGS) -MMD -MP -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+-include $(DEPS)
 
 clean:
 	rm -rf build $(LIB)

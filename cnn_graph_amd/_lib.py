@@ -46,6 +46,14 @@ _SIGNATURES = {
                         _c_int),
     "cg_cheb_backward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_sz,
                           _vp], _c_int),
+    "cg_weight_grad_workspace_bytes": ([_c_i64, _c_i32, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
+    "cg_weight_grad": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
+    "cg_bias_grad_workspace_bytes": ([_c_i64, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
+    "cg_bias_grad": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
+    "cg_lstm_cell_forward": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+                             _c_int),
+    "cg_lstm_cell_backward": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+                              _c_int),
     "cg_perm_gather": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
     "cg_maxpool_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp], _c_int),
     "cg_maxpool_backward": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),

@@ -168,6 +168,23 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
 int gemm_effective_splits(int Kg, int splits);
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,
                                hipStream_t s);
+// Same fixed-order reduction, then out[i] = out[i] + sum (accumulate != 0).
+hipError_t launch_reduce_slabs_acc(const float* slab, int nslab, int64_t count, float* out,
+                                   int accumulate, hipStream_t s);
+
+// ---- gconv-LSTM cell (lstm.hip) ------------------------------------------------
+// gates: 0 = reference gate functions (tan / sigmoid / sigmoid / tanh,
+// lib/gconv_lstm.py:188-209), 1 = standard LSTM (tanh / ... / sigmoid).
+hipError_t launch_lstm_fwd(int gates, int64_t R, int H, const float* gx, const float* gh,
+                           const float* bias, const float* c, float* c_out, float* h_out,
+                           float* act, hipStream_t s);
+hipError_t launch_lstm_bwd(int gates, int64_t R, int H, const float* dh, const float* dh_rec,
+                           const float* dc,
+                           const float* act, const float* c, const float* c_out, float* dpre,
+                           float* dc_prev, hipStream_t s);
+// Column sums of A [R][C] as [colsum_chunks(R)][C] partial slabs.
+int colsum_chunks(int64_t R);
+hipError_t launch_colsum_slabs(const float* A, int64_t R, int C, float* slab, hipStream_t s);
 
 // ---- misc ----------------------------------------------------------------------
 hipError_t launch_perm_gather(const float* x, const int32_t* perm, int N, int M_in, int M_out,

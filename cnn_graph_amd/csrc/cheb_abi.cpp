@@ -365,7 +365,7 @@ int ensure_side_stream(cg_plan* p) {
 
 extern "C" {
 
-int cg_version(void) { return 100; }
+int cg_version(void) { return 200; }
 
 // Timing-ablation hook (not in the public header; outputs are WRONG when set).
 int cg_debug_set_flags(int flags) {
@@ -586,7 +586,8 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
                      void* workspace, size_t ws_bytes, void* stream) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
-  if (!dy || !basis || !W || !dW) return fail(CG_ERR_ARG, "null dy/basis/W/dW");
+  if (!dy || !basis || !W) return fail(CG_ERR_ARG, "null dy/basis/W");
+  if (!dx && !dW) return fail(CG_ERR_ARG, "dx and dW are both NULL: nothing to compute");
   if ((rc = check_device(plan))) return rc;
   int path = 0;
   if ((rc = choose_path(plan, Fin, K, Fout, true, &path))) return rc;
@@ -616,7 +617,8 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
     CG_HIP(hipEventRecord(plan->ev_fork, s));
     CG_HIP(hipStreamWaitEvent(plan->side, plan->ev_fork, 0));
   }
-  const bool fused = dx != nullptr && path == CG_PATH_RESIDENT && fused_dw(plan, Fin, K, Fout);
+  const bool fused =
+      dx != nullptr && dW != nullptr && path == CG_PATH_RESIDENT && fused_dw(plan, Fin, K, Fout);
   if (dx) {
     if (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, true)) {
       const cg::FastGeom g = fast_geom(plan, Fin, K, Fout);
@@ -666,6 +668,7 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
                                         G(k), dA, dx, N, M, Fin, K, k, s));
     }
   }
+  if (!dW) return ok();
   if (!fused && !(cg::g_debug_flags & (1 << 22)))  // ablation hook: skip dW
     CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, sdw));
   if (overlap) {
@@ -674,6 +677,78 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
   }
   if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
     CG_HIP(cg::launch_reduce_slabs(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, s));
+  return ok();
+}
+
+int cg_weight_grad_workspace_bytes(int64_t R, int32_t FinK, int32_t Fout, size_t* bytes) {
+  if (!bytes || R < 1 || FinK < 1 || Fout < 1) return fail(CG_ERR_ARG, "weight_grad: bad arguments");
+  *bytes = dw_slab_bytes(R, 0, FinK, Fout);
+  return ok();
+}
+
+int cg_weight_grad(int64_t R, int32_t FinK, int32_t Fout, const float* basis, const float* dy,
+                   float* dW, int32_t accumulate, void* workspace, size_t ws_bytes, void* stream) {
+  if (!basis || !dy || !dW || R < 1 || FinK < 1 || Fout < 1)
+    return fail(CG_ERR_ARG, "weight_grad: bad arguments");
+  const size_t need = dw_slab_bytes(R, 0, FinK, Fout);
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "weight_grad workspace too small: %zu < %zu", ws_bytes, need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* slabs = static_cast<float*>(workspace);
+  CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, s));
+  CG_HIP(cg::launch_reduce_slabs_acc(slabs, cg::dw_chunks(R), int64_t(FinK) * Fout, dW,
+                                     accumulate != 0, s));
+  return ok();
+}
+
+int cg_bias_grad_workspace_bytes(int64_t R, int32_t C, size_t* bytes) {
+  if (!bytes || R < 1 || C < 1) return fail(CG_ERR_ARG, "bias_grad: bad arguments");
+  *bytes = al256(size_t(cg::colsum_chunks(R)) * size_t(C) * 4);
+  return ok();
+}
+
+int cg_bias_grad(int64_t R, int32_t C, const float* dy, float* db, int32_t accumulate,
+                 void* workspace, size_t ws_bytes, void* stream) {
+  if (!dy || !db || R < 1 || C < 1) return fail(CG_ERR_ARG, "bias_grad: bad arguments");
+  const size_t need = al256(size_t(cg::colsum_chunks(R)) * size_t(C) * 4);
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "bias_grad workspace too small: %zu < %zu", ws_bytes, need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* slabs = static_cast<float*>(workspace);
+  CG_HIP(cg::launch_colsum_slabs(dy, R, C, slabs, s));
+  CG_HIP(cg::launch_reduce_slabs_acc(slabs, cg::colsum_chunks(R), C, db, accumulate != 0, s));
+  return ok();
+}
+
+static int check_lstm(int64_t R, int32_t H, int32_t gates) {
+  if (R < 1 || H < 1) return fail(CG_ERR_ARG, "lstm: bad shape R=%lld H=%d", (long long)R, H);
+  if (R * int64_t(H) * 4 >= (int64_t(1) << 31))
+    return fail(CG_ERR_ARG, "lstm: R*4H = %lld exceeds 2^31", (long long)(R * H * 4));
+  if (gates != CG_LSTM_GATES_REFERENCE && gates != CG_LSTM_GATES_STANDARD)
+    return fail(CG_ERR_ARG, "lstm: unknown gate set %d", gates);
+  return CG_OK;
+}
+
+int cg_lstm_cell_forward(int64_t R, int32_t H, int32_t gates, const float* gx, const float* gh,
+                         const float* bias, const float* c, float* c_out, float* h_out, float* act,
+                         void* stream) {
+  int rc = check_lstm(R, H, gates);
+  if (rc) return rc;
+  if (!gx || !c_out || !h_out) return fail(CG_ERR_ARG, "lstm_cell_forward: null gx/c_out/h_out");
+  CG_HIP(cg::launch_lstm_fwd(gates, R, H, gx, gh, bias, c, c_out, h_out, act,
+                             reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_lstm_cell_backward(int64_t R, int32_t H, int32_t gates, const float* dh,
+                          const float* dh_rec, const float* dc,
+                          const float* act, const float* c, const float* c_out, float* dpre,
+                          float* dc_prev, void* stream) {
+  int rc = check_lstm(R, H, gates);
+  if (rc) return rc;
+  if (!act || !c_out || !dpre) return fail(CG_ERR_ARG, "lstm_cell_backward: null act/c_out/dpre");
+  CG_HIP(cg::launch_lstm_bwd(gates, R, H, dh, dh_rec, dc, act, c, c_out, dpre, dc_prev,
+                             reinterpret_cast<hipStream_t>(stream)));
   return ok();
 }
 

@@ -250,7 +250,8 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
 // 256-B coalesced load per slab, 8 in flight), then the 16 partial sums are
 // added in wave order through LDS.
 __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__ slab, int nslab,
-                                                       int64_t count, float* __restrict__ out) {
+                                                       int64_t count, float* __restrict__ out,
+                                                       int accumulate) {
 #pragma clang fp contract(off)
   __shared__ float part[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
     float t = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) t = t + part[q][lane];
-    out[i] = t;
+    out[i] = accumulate ? out[i] + t : t;
   }
 }
 
@@ -355,8 +356,13 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
 
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,
                                hipStream_t s) {
+  return launch_reduce_slabs_acc(slab, nslab, count, out, 0, s);
+}
+
+hipError_t launch_reduce_slabs_acc(const float* slab, int nslab, int64_t count, float* out,
+                                   int accumulate, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce_slabs, dim3(unsigned((count + 63) / 64)), dim3(1024), 0, s, slab,
-                     nslab, count, out);
+                     nslab, count, out, accumulate);
   return hipGetLastError();
 }
 

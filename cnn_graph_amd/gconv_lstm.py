@@ -1,0 +1,267 @@
+"""gconv-LSTM on the HIP Chebyshev path: drop-in for ``lib/gconv_lstm.py``'s
+``GConvLSTMCell`` (lib/gconv_lstm.py:29-221) and the ``static_rnn`` over a
+``MultiRNNCell`` that ``GconvModel.glstm_layer`` builds (:609-627).
+
+Reference behaviour kept:
+  * eight ``cheby_conv`` weights ``W{z,i,f,o}{x,h}t`` of shape [K*feat_in, H]
+    and [K*H, H], ``random_uniform(-0.1, 0.1)`` (:98-115), and four biases
+    ``b{z,i,f,o}t`` [H] with ``tf.get_variable``'s default (Glorot-uniform)
+    initialiser (:173-176); ``K`` defaults to 2 (:95-96);
+  * gate functions z = tan, i = f = sigmoid, o = tanh (:188, :195, :202, :209)
+    -- ``gates="standard"`` gives the usual tanh / sigmoid instead;
+  * ``forget_bias`` is accepted and ignored, as in the reference (:49);
+  * ``__call__(inputs, state) -> (new_h, LSTMStateTuple(new_c, new_h))``.
+  * ``DropoutWrapper(output_keep_prob=0.8)`` (:616, :623) is NOT applied: it is
+    training-time noise outside the filter path (pass ``keep_prob`` to
+    ``static_rnn`` callers' own dropout if needed).
+
+MI355X design: the four x-weights (and the four h-weights) are stored
+concatenated as one [K*F, 4H] matrix, so a cell step is TWO chebyshev5 calls
+(one Chebyshev basis of x, one of h) plus one fused pointwise kernel, not the
+reference's eight filters.  ``static_rnn`` additionally batches the x-conv of
+ALL time steps into one call (it does not depend on the recurrence), runs the
+T h-convs back to back, and in the backward sums the h-weight gradient of all
+steps with one ``cg_weight_grad`` over the stacked bases.
+"""
+from __future__ import annotations
+
+import collections
+import math
+
+import torch
+
+from . import ops
+from .plan import plan_for
+
+_LSTMStateTuple = collections.namedtuple("LSTMStateTuple", ("c", "h"))
+
+
+class LSTMStateTuple(_LSTMStateTuple):
+    """(c, h) -- lib/gconv_lstm.py:16-26."""
+    __slots__ = ()
+
+    @property
+    def dtype(self):
+        c, h = self
+        if c.dtype != h.dtype:
+            raise TypeError("Inconsistent internal state")
+        return c.dtype
+
+
+GATE_NAMES = ("z", "i", "f", "o")
+
+
+class GConvLSTMCell:
+    """lib/gconv_lstm.py:29-221 on the HIP kernels.  Parameters live in
+    ``Wx`` [K*feat_in, 4H], ``Wh`` [K*H, 4H], ``b`` [4H]; ``variables`` maps the
+    reference's variable names (``Wzxt``, ``Wiht``, ``bft``, ...) to views."""
+
+    def __init__(self, num_units, forget_bias=1.0, state_is_tuple=True, activation=None,
+                 reuse=None, laplacian=None, lmax=None, K=None, feat_in=None, nNode=None,
+                 filter_type="cheby_conv", gates="reference", device=None, generator=None):
+        if filter_type != "cheby_conv":
+            raise NotImplementedError(f"filter_type={filter_type!r}: only the Chebyshev filter "
+                                      "is on the MI355X path (fourier_conv is out of scope)")
+        if laplacian is None or feat_in is None:
+            raise ValueError("laplacian and feat_in are required")
+        if gates not in ops.LSTM_GATES:
+            raise ValueError(f"gates must be one of {list(ops.LSTM_GATES)}")
+        self._num_units = H = int(num_units)
+        self._forget_bias = forget_bias          # unused, as in the reference
+        self._state_is_tuple = state_is_tuple
+        self._laplacian = laplacian
+        self._lmax = 2 if lmax is None else lmax  # graph.lmax(normalized L) == 2
+        self._K = 2 if K is None else int(K)      # :95-96
+        self._feat_in = int(feat_in)
+        self._nNode = int(nNode) if nNode is not None else int(laplacian.shape[0])
+        self.gates = gates
+        self.device = torch.device(device if device is not None else "cuda")
+        dev_index = self.device.index if self.device.index is not None else 0
+        self.plan = plan_for(laplacian, lmax=self._lmax, device=dev_index)
+        K, F = self._K, self._feat_in
+        f32 = dict(device=self.device, dtype=torch.float32)
+        with torch.no_grad():
+            Wx = torch.empty((K * F, 4 * H), **f32).uniform_(-0.1, 0.1, generator=generator)
+            Wh = torch.empty((K * H, 4 * H), **f32).uniform_(-0.1, 0.1, generator=generator)
+            lim = math.sqrt(6.0 / (H + H))  # glorot_uniform of a [H] vector: fan_in = fan_out = H
+            b = torch.empty((4 * H,), **f32).uniform_(-lim, lim, generator=generator)
+        self.Wx = torch.nn.Parameter(Wx)
+        self.Wh = torch.nn.Parameter(Wh)
+        self.b = torch.nn.Parameter(b)
+
+    # -- reference properties ---------------------------------------------------
+    @property
+    def state_size(self):
+        if self._state_is_tuple:
+            return LSTMStateTuple((self._nNode, self._num_units), (self._nNode, self._num_units))
+        return 2 * self._num_units
+
+    @property
+    def output_size(self):
+        return self._num_units
+
+    @property
+    def variables(self):
+        H = self._num_units
+        v = {}
+        for q, g in enumerate(GATE_NAMES):
+            sl = slice(q * H, (q + 1) * H)
+            v[f"W{g}xt"] = self.Wx[:, sl]
+            v[f"W{g}ht"] = self.Wh[:, sl]
+            v[f"b{g}t"] = self.b[sl]
+        return v
+
+    def parameters(self):
+        return [self.Wx, self.Wh, self.b]
+
+    def zero_state(self, batch_size, dtype=torch.float32):
+        """(c, h) zeros of [batch, nNode, H] (lib/gconv_lstm.py:71-76)."""
+        shape = (int(batch_size), self._nNode, self._num_units)
+        return (torch.zeros(shape, device=self.device, dtype=dtype),
+                torch.zeros(shape, device=self.device, dtype=dtype))
+
+    # -- one step (lib/gconv_lstm.py:77-221) -----------------------------------------
+    def __call__(self, inputs, state, scope=None):
+        if self._state_is_tuple:
+            c, h = state
+        else:
+            c, h = torch.split(state, self._nNode, dim=1)  # tf.split(state, 2, axis=1) (:82)
+        new_c, new_h = _CellStep.apply(inputs, c, h, self.Wx, self.Wh, self.b, self)
+        if self._state_is_tuple:
+            new_state = LSTMStateTuple(new_c, new_h)
+        else:
+            new_state = torch.cat([new_c, new_h], 1)  # tf.concat([new_c, new_h], 1) (:220)
+        return new_h, new_state
+
+
+class _CellStep(torch.autograd.Function):
+    """One cell step: x-conv, h-conv (4 gates each, one basis per input),
+    fused gates; backward = gates backward, two chebyshev5 backwards, bias sum."""
+
+    @staticmethod
+    def forward(ctx, x, c, h, Wx, Wh, b, cell: GConvLSTMCell):
+        H, K = cell._num_units, cell._K
+        plan = cell.plan
+        x, c, h = x.contiguous(), c.contiguous(), h.contiguous()
+        basis_x, gx = ops.cheb_forward(plan, x, Wx, K)
+        basis_h, gh = ops.cheb_forward(plan, h, Wh, K)
+        c_out, h_out, act = ops.lstm_cell_forward(gx, gh, b, c, H, cell.gates)
+        ctx.save_for_backward(basis_x, basis_h, Wx, Wh, act, c, c_out)
+        ctx.cell = cell
+        return c_out, h_out
+
+    @staticmethod
+    def backward(ctx, dc_out, dh_out):
+        basis_x, basis_h, Wx, Wh, act, c, c_out = ctx.saved_tensors
+        cell = ctx.cell
+        H, K, plan = cell._num_units, cell._K, cell.plan
+        dh = dh_out.contiguous() if dh_out is not None else None
+        dc = dc_out.contiguous() if dc_out is not None else None
+        dpre, dc_prev = ops.lstm_cell_backward(dh, None, dc, act, c, c_out, H, cell.gates)
+        dx, dWx = ops.cheb_backward(plan, dpre, basis_x, Wx, K, need_dx=ctx.needs_input_grad[0])
+        dh_prev, dWh = ops.cheb_backward(plan, dpre, basis_h, Wh, K)
+        db = ops.bias_grad(dpre)
+        return dx, dc_prev, dh_prev, dWx, dWh, db, None
+
+
+class _Layer(torch.autograd.Function):
+    """static_rnn of one cell over a [T, N, M, F] sequence (time-batched x-conv,
+    T h-convs, BPTT with one weight-gradient GEMM for the h-weights)."""
+
+    @staticmethod
+    def forward(ctx, xs, c0, h0, Wx, Wh, b, cell: GConvLSTMCell, zero_init: bool):
+        H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
+        xs = xs.contiguous()
+        T, N, M, F = xs.shape
+        R = N * M
+        dev = xs.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        # x-conv of every step at once: a batch of T*N samples
+        basis_x, gx = ops.cheb_forward(plan, xs.view(T * N, M, F), Wx, K)
+        gx = gx.view(T, R, 4 * H)
+        hs = torch.empty((T, N, M, H), **f32)
+        cs = torch.empty((T, N, M, H), **f32)
+        act = torch.empty((T, R, 4 * H), **f32)
+        basis_h = torch.empty((T, R, H * K), **f32)
+        gh = torch.empty((N, M, 4 * H), **f32)
+        for t in range(T):
+            h_prev = (None if zero_init else h0) if t == 0 else hs[t - 1]
+            c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
+            if h_prev is not None:
+                ops.cheb_forward(plan, h_prev, Wh, K, out_basis=basis_h[t], out_y=gh)
+            ops.lstm_cell_forward(gx[t], gh if h_prev is not None else None, b, c_prev, H, gates,
+                                  out_c=cs[t], out_h=hs[t], out_act=act[t])
+        ctx.save_for_backward(basis_x, basis_h, Wx, Wh, act, cs, c0, h0)
+        ctx.cell, ctx.zero_init, ctx.shape = cell, zero_init, (T, N, M, F)
+        return hs, cs[T - 1].clone()
+
+    @staticmethod
+    def backward(ctx, dhs, dcT):
+        basis_x, basis_h, Wx, Wh, act, cs, c0, _h0 = ctx.saved_tensors
+        cell, zero_init = ctx.cell, ctx.zero_init
+        H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
+        T, N, M, F = ctx.shape
+        R = N * M
+        dev = act.device
+        dpre = torch.empty((T, R, 4 * H), device=dev, dtype=torch.float32)
+        dhs = dhs.contiguous() if dhs is not None else None
+        dc = dcT.contiguous() if dcT is not None else None
+        dh_rec = None
+        t_first = 1 if zero_init else 0  # first step whose h-conv ran
+        for t in range(T - 1, -1, -1):
+            c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
+            dpre_t, dc = ops.lstm_cell_backward(None if dhs is None else dhs[t], dh_rec, dc, act[t],
+                                                c_prev, cs[t], H, gates, out_dpre=dpre[t])
+            if t >= t_first:
+                dh_rec, _ = ops.cheb_backward(plan, dpre[t].view(N, M, 4 * H),
+                                              basis_h[t].view(R, H * K), Wh, K, need_dW=False)
+            else:
+                dh_rec = None
+        dWh = (ops.weight_grad(basis_h[t_first:], dpre[t_first:]) if T > t_first
+               else torch.zeros_like(Wh))
+        dxs, dWx = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), basis_x, Wx, K,
+                                     need_dx=ctx.needs_input_grad[0])
+        db = ops.bias_grad(dpre)
+        dx_out = dxs.view(T, N, M, F) if dxs is not None else None
+        dc0 = None if zero_init else dc
+        dh0 = None if zero_init else dh_rec
+        return dx_out, dc0, dh0, dWx, dWh, db, None, None
+
+
+def layer(cell: GConvLSTMCell, xs: torch.Tensor, initial_state=None):
+    """Run ``cell`` over xs [T, N, M, feat_in]; returns (hs [T, N, M, H],
+    LSTMStateTuple(c_T, h_T)).  initial_state None = zero state."""
+    if initial_state is None:
+        z = xs.new_zeros(())
+        hs, cT = _Layer.apply(xs, z, z, cell.Wx, cell.Wh, cell.b, cell, True)
+    else:
+        c0, h0 = initial_state
+        hs, cT = _Layer.apply(xs, c0.contiguous(), h0.contiguous(), cell.Wx, cell.Wh, cell.b, cell,
+                              False)
+    return hs, LSTMStateTuple(cT, hs[-1])
+
+
+def static_rnn(cells, inputs, initial_states=None):
+    """``tf.nn.static_rnn(MultiRNNCell(cells), inputs)`` (lib/gconv_lstm.py:625-626).
+
+    inputs: a list of T tensors [N, M, F] or one [T, N, M, F] tensor.
+    Returns (outputs: list of T tensors [N, M, H] of the last layer,
+    states: tuple of LSTMStateTuple per layer).  Layer-by-layer evaluation
+    equals the reference's time-major one (layer l at step t depends only on
+    layer l-1 at step t and layer l at step t-1)."""
+    if isinstance(cells, GConvLSTMCell):
+        cells = [cells]
+    xs = torch.stack(list(inputs)) if isinstance(inputs, (list, tuple)) else inputs
+    states = []
+    for li, cell in enumerate(cells):
+        init = None if initial_states is None else initial_states[li]
+        xs, st = layer(cell, xs, init)
+        states.append(st)
+    return list(xs.unbind(0)), tuple(states)
+
+
+def unstack_time(x: torch.Tensor, T: int) -> torch.Tensor:
+    """inference_glstm's split (lib/gconv_lstm.py:272-275): [N, M, F*T] ->
+    reshape [N, M, F, T] -> unstack axis 3 -> [T, N, M, F] (contiguous)."""
+    N, M, C = x.shape
+    return x.reshape(N, M, C // T, T).permute(3, 0, 1, 2).contiguous()

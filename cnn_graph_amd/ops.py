@@ -12,6 +12,8 @@ or a missing library raises.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -34,9 +36,22 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def _check_out(name, t, shape):
+    """A caller-supplied output: fp32, on the GPU, contiguous, with prod(shape) elements."""
+    _check_dev(name, t)
+    n = 1
+    for s in shape:
+        n *= int(s)
+    if not t.is_contiguous() or t.numel() != n:
+        raise ValueError(f"{name}: need a contiguous tensor of {tuple(shape)} elements, "
+                         f"got {tuple(t.shape)}")
+
+
 def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int,
-                 want_basis: bool = True):
-    """Basis (N*M, Fin*K) and y = basis @ W (N, M, Fout).  W None -> basis only."""
+                 want_basis: bool = True, out_basis: torch.Tensor | None = None,
+                 out_y: torch.Tensor | None = None):
+    """Basis (N*M, Fin*K) and y = basis @ W (N, M, Fout).  W None -> basis only.
+    out_basis / out_y: pre-allocated contiguous outputs of those shapes."""
     _check_dev("x", x)
     x = x.contiguous()
     N, M, Fin = x.shape
@@ -53,8 +68,14 @@ def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int
     dev = x.device
     # the streaming path's GEMM reads the basis from HBM, so it always needs one
     need_basis = want_basis or W is None or plan.query_path(N, Fin, K, Fout) == "stream"
-    basis = torch.empty((N * M, Fin * K), device=dev, dtype=torch.float32) if need_basis else None
-    y = torch.empty((N, M, Fout), device=dev, dtype=torch.float32) if W is not None else None
+    basis = y = None
+    if need_basis:
+        basis = out_basis if out_basis is not None else torch.empty((N * M, Fin * K), device=dev,
+                                                                    dtype=torch.float32)
+        _check_out("out_basis", basis, (N * M, Fin * K))
+    if W is not None:
+        y = out_y if out_y is not None else torch.empty((N, M, Fout), device=dev, dtype=torch.float32)
+        _check_out("out_y", y, (N * M * Fout,))
     fwd_ws, _ = plan.workspace_bytes(N, Fin, K, Fout)
     ws = torch.empty(max(fwd_ws, 1), device=dev, dtype=torch.uint8)
     _lib.call("cg_cheb_forward", plan.handle, N, Fin, K, Fout, _p(x), _p(W), _p(basis), _p(y),
@@ -63,8 +84,8 @@ def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int
 
 
 def cheb_backward(plan: ChebPlan, dy: torch.Tensor, basis: torch.Tensor, W: torch.Tensor, K: int,
-                  need_dx: bool = True):
-    """(dx [N,M,Fin] or None, dW [Fin*K, Fout])."""
+                  need_dx: bool = True, need_dW: bool = True):
+    """(dx [N,M,Fin] or None, dW [Fin*K, Fout] or None)."""
     _check_dev("dy", dy)
     dy = dy.contiguous()
     N, M, Fout = dy.shape
@@ -72,7 +93,7 @@ def cheb_backward(plan: ChebPlan, dy: torch.Tensor, basis: torch.Tensor, W: torc
     Fin = FinK // K
     dev = dy.device
     dx = torch.empty((N, M, Fin), device=dev, dtype=torch.float32) if need_dx else None
-    dW = torch.empty((FinK, Fout), device=dev, dtype=torch.float32)
+    dW = torch.empty((FinK, Fout), device=dev, dtype=torch.float32) if need_dW else None
     _, bwd_ws = plan.workspace_bytes(N, Fin, K, Fout)
     ws = torch.empty(max(bwd_ws, 1), device=dev, dtype=torch.uint8)
     _lib.call("cg_cheb_backward", plan.handle, N, Fin, K, Fout, _p(dy), _p(basis), _p(W.contiguous()),
@@ -217,6 +238,98 @@ def perm_data(x: torch.Tensor, perm) -> torch.Tensor:
     out = torch.empty((N, Mo, F), device=x.device, dtype=torch.float32)
     _lib.call("cg_perm_gather", _p(x3), _p(perm_t), N, M, Mo, F, _p(out), _stream(x))
     return out[..., 0] if squeeze else out
+
+
+def weight_grad(basis: torch.Tensor, dy: torch.Tensor, out: torch.Tensor | None = None,
+                accumulate: bool = False) -> torch.Tensor:
+    """dW = basis^T dy over all rows (basis [R, FinK], dy [R, Fout] in any
+    [..., Fout] shape); accumulate=True adds into ``out``."""
+    _check_dev("basis", basis)
+    _check_dev("dy", dy)
+    FinK = int(basis.shape[-1])
+    R = basis.numel() // FinK
+    Fout = int(dy.shape[-1])
+    if dy.numel() != R * Fout:
+        raise ValueError(f"dy has {dy.numel()} elements, expected R*Fout = {R * Fout}")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate=True needs an out tensor")
+        out = torch.empty((FinK, Fout), device=basis.device, dtype=torch.float32)
+    _check_out("out", out, (FinK, Fout))
+    nb = ctypes.c_size_t()
+    _lib.call("cg_weight_grad_workspace_bytes", R, FinK, Fout, ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 1), device=basis.device, dtype=torch.uint8)
+    _lib.call("cg_weight_grad", R, FinK, Fout, _p(basis.contiguous()), _p(dy.contiguous()), _p(out),
+              int(accumulate), _p(ws), nb.value, _stream(basis))
+    return out
+
+
+def bias_grad(dy: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):
+    """db = dy summed over every axis but the last (gradient of a broadcast bias)."""
+    _check_dev("dy", dy)
+    C = int(dy.shape[-1])
+    R = dy.numel() // C
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate=True needs an out tensor")
+        out = torch.empty((C,), device=dy.device, dtype=torch.float32)
+    _check_out("out", out, (C,))
+    nb = ctypes.c_size_t()
+    _lib.call("cg_bias_grad_workspace_bytes", R, C, ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 1), device=dy.device, dtype=torch.uint8)
+    _lib.call("cg_bias_grad", R, C, _p(dy.contiguous()), _p(out), int(accumulate), _p(ws), nb.value,
+              _stream(dy))
+    return out
+
+
+LSTM_GATES = {"reference": 0, "standard": 1}
+
+
+def lstm_cell_forward(gx, gh, bias, c, H: int, gates="reference", out_c=None, out_h=None,
+                      out_act=None):
+    """Pointwise part of GConvLSTMCell (lib/gconv_lstm.py:183-221): gx, gh
+    [..., 4H] gate pre-activations of the x- and h-conv (gh None = 0), bias
+    [4H] (None = 0), c [..., H] (None = 0).  Returns (c', h', act [..., 4H])."""
+    _check_dev("gx", gx)
+    R = gx.numel() // (4 * H)
+    lead = tuple(gx.shape[:-1])
+    dev = gx.device
+    for name, t, n in (("gh", gh, 4 * H), ("bias", bias, 4 * H), ("c", c, H)):
+        if t is not None:
+            _check_dev(name, t)
+            if not t.is_contiguous() or t.numel() != (n if name == "bias" else R * n):
+                raise ValueError(f"{name}: bad shape {tuple(t.shape)}")
+    c_out = out_c if out_c is not None else torch.empty(lead + (H,), device=dev, dtype=torch.float32)
+    h_out = out_h if out_h is not None else torch.empty(lead + (H,), device=dev, dtype=torch.float32)
+    act = out_act if out_act is not None else torch.empty(lead + (4 * H,), device=dev,
+                                                          dtype=torch.float32)
+    _check_out("c_out", c_out, (R, H))
+    _check_out("h_out", h_out, (R, H))
+    _check_out("act", act, (R, 4 * H))
+    _lib.call("cg_lstm_cell_forward", R, H, LSTM_GATES[gates], _p(gx.contiguous()), _p(gh), _p(bias),
+              _p(c), _p(c_out), _p(h_out), _p(act), _stream(gx))
+    return c_out, h_out, act
+
+
+def lstm_cell_backward(dh, dh_rec, dc, act, c, c_out, H: int, gates="reference", out_dpre=None,
+                       need_dc_prev=True):
+    """Backward of lstm_cell_forward: (dpre [..., 4H], dc_prev [..., H] or None)."""
+    _check_dev("act", act)
+    _check_dev("c_out", c_out)
+    R = act.numel() // (4 * H)
+    dev = act.device
+    for name, t in (("dh", dh), ("dh_rec", dh_rec), ("dc", dc), ("c", c)):
+        if t is not None:
+            _check_dev(name, t)
+            if not t.is_contiguous() or t.numel() != R * H:
+                raise ValueError(f"{name}: bad shape {tuple(t.shape)}")
+    dpre = out_dpre if out_dpre is not None else torch.empty(tuple(act.shape), device=dev,
+                                                             dtype=torch.float32)
+    _check_out("dpre", dpre, (R, 4 * H))
+    dc_prev = torch.empty(tuple(c_out.shape), device=dev, dtype=torch.float32) if need_dc_prev else None
+    _lib.call("cg_lstm_cell_backward", R, H, LSTM_GATES[gates], _p(dh), _p(dh_rec), _p(dc), _p(act),
+              _p(c), _p(c_out), _p(dpre), _p(dc_prev), _stream(act))
+    return dpre, dc_prev
 
 
 def adam_update(param, grad, m, v, step: int, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,

@@ -98,12 +98,57 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
 /* ---------------------------------------------------------------------------
  * Backward (TF autodiff of the above via lib/graph_model.py:296):
  *   dy [N][M][Fout], basis (from forward), W  ->
- *   dx [N][M][Fin]  (NULL to skip), dW [Fin*K][Fout]  (overwritten, not accumulated)
+ *   dx [N][M][Fin]  (NULL to skip), dW [Fin*K][Fout]  (overwritten, not accumulated;
+ *   NULL to skip -- e.g. a recurrent caller that sums dW over time steps with
+ *   one cg_weight_grad call; dx and dW may not both be NULL)
  * dW = basis^T dy ; dBasis = dy W^T ; reverse recurrence over L~^T.
  * ------------------------------------------------------------------------- */
 int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                      const float* dy, const float* basis, const float* W,
                      float* dx, float* dW, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Weight gradient of the contraction on its own (the tf.matmul gradient of
+ * lib/graph_conv.py:175 / lib/filter.py:93): dW = basis^T dy over R rows,
+ * basis [R][FinK], dy [R][Fout], dW [FinK][Fout].  Fixed-order, bitwise
+ * reproducible reduction; accumulate != 0 adds into dW (dW += ...), so
+ * recurrent callers can sum the gradient of a weight shared over time steps.
+ * ------------------------------------------------------------------------- */
+int cg_weight_grad_workspace_bytes(int64_t R, int32_t FinK, int32_t Fout, size_t* bytes);
+int cg_weight_grad(int64_t R, int32_t FinK, int32_t Fout, const float* basis, const float* dy,
+                   float* dW, int32_t accumulate, void* workspace, size_t ws_bytes, void* stream);
+/* db[c] (+)= sum_r dy[r][c] -- gradient of a broadcast bias add, dy [R][C]. */
+int cg_bias_grad_workspace_bytes(int64_t R, int32_t C, size_t* bytes);
+int cg_bias_grad(int64_t R, int32_t C, const float* dy, float* db, int32_t accumulate,
+                 void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * gconv-LSTM cell pointwise part (lib/gconv_lstm.py:77-221, GConvLSTMCell).
+ * The cell's eight cheby_conv calls are two chebyshev5 calls with the four
+ * gate weights concatenated: gx = cheb(x; [Wzxt|Wixt|Wfxt|Woxt]) and
+ * gh = cheb(h; [Wzht|Wiht|Wfht|Woht]), each [R][4H] with R = N*M rows and
+ * gate blocks z | i | f | o of H columns.  Then per (r, j):
+ *   a_q = (gx_q + gh_q) + b_q                      (:186, :193, :200, :207)
+ *   REFERENCE gates: z = tan(a_z), i = sigmoid, f = sigmoid, o = tanh(a_o)
+ *   STANDARD gates:  z = tanh(a_z), o = sigmoid(a_o)
+ *   c' = f*c + i*z ;  h' = o*tanh(c')              (:215, :218)
+ * gh, bias, c may be NULL (zero: the zero state of :71-76).  act [R][4H]
+ * receives the gate activations (z|i|f|o) for the backward; may be NULL.
+ * ------------------------------------------------------------------------- */
+enum { CG_LSTM_GATES_REFERENCE = 0, CG_LSTM_GATES_STANDARD = 1 };
+int cg_lstm_cell_forward(int64_t R, int32_t H, int32_t gates, const float* gx, const float* gh,
+                         const float* bias, const float* c, float* c_out, float* h_out, float* act,
+                         void* stream);
+/* Backward of the pointwise part: dh + dh_rec = gradient w.r.t. h' (the
+ * step's output gradient and the recurrent one from step t+1's h-conv,
+ * summed in-kernel), dc = gradient w.r.t. c' (any of the three NULL = 0);
+ * act, c (NULL = 0), c_out from the forward.  Writes
+ * dpre [R][4H] = dLoss/d(a_z | a_i | a_f | a_o) (the dy of both gate
+ * contractions and of the bias) and dc_prev [R][H] = dLoss/dc (NULL to skip). */
+int cg_lstm_cell_backward(int64_t R, int32_t H, int32_t gates, const float* dh,
+                          const float* dh_rec, const float* dc,
+                          const float* act, const float* c, const float* c_out, float* dpre,
+                          float* dc_prev, void* stream);
 
 /* ---------------------------------------------------------------------------
  * perm_data (lib/coarsening.py:219-240) on device:

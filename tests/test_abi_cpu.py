@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol(built_lib):
 
 
 def test_version(built_lib):
-    assert _lib.lib().cg_version() == 100
+    assert _lib.lib().cg_version() == 200
 
 
 def _i32(a):
@@ -53,3 +53,21 @@ def test_null_and_shape_errors(built_lib):
     assert h.cg_adam_update(None, None, None, None, 1, 0.1, 0.9, 0.999, 1e-8, 0, 1.0, None) == _lib.CG_ERR_ARG
     with pytest.raises(_lib.CGError):
         _lib.call("cg_plan_set_path", None, 0)
+
+
+def test_lstm_and_grad_entry_points_validate(built_lib):
+    h = _lib.lib()
+    sz = ctypes.c_size_t()
+    assert h.cg_weight_grad_workspace_bytes(1000, 96, 128, ctypes.byref(sz)) == _lib.CG_OK
+    assert sz.value >= 96 * 128 * 4
+    assert h.cg_bias_grad_workspace_bytes(1000, 128, ctypes.byref(sz)) == _lib.CG_OK
+    assert sz.value >= 128 * 4
+    assert h.cg_weight_grad(0, 96, 128, None, None, None, 0, None, 0, None) == _lib.CG_ERR_ARG
+    assert h.cg_bias_grad(10, 4, None, None, 0, None, 0, None) == _lib.CG_ERR_ARG
+    # unknown gate set / null operands are rejected before any launch
+    assert h.cg_lstm_cell_forward(4, 2, 7, 1, None, None, None, 1, 1, None, None) == _lib.CG_ERR_ARG
+    assert "gate" in h.cg_last_error().decode()
+    assert h.cg_lstm_cell_forward(4, 2, 0, None, None, None, None, None, None, None, None) == _lib.CG_ERR_ARG
+    assert h.cg_lstm_cell_backward(4, 2, 0, None, None, None, None, None, None, None, None, None) == _lib.CG_ERR_ARG
+    assert h.cg_lstm_cell_forward(1 << 30, 8, 0, 1, None, None, None, 1, 1, None, None) == _lib.CG_ERR_ARG
+    assert "2^31" in h.cg_last_error().decode()

@@ -1,0 +1,230 @@
+"""gconv-LSTM cell (lib/gconv_lstm.py:77-221) on the HIP path vs the float64
+oracle (oracle/lstm_oracle.py).  Bar: max-abs-normalised error <= 1e-5
+(the north star's 1e-5 rel-fp32), on forward states and every gradient."""
+import numpy as np
+import pytest
+import scipy.sparse
+
+from conftest import case, load_golden
+from oracle import cheb_oracle as O
+from oracle import lstm_oracle as LO
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def dev(built_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_graph_amd import _lib
+    _lib.lib()
+    return torch.device("cuda", 0)
+
+
+def t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+
+
+def graph_E():
+    """config E's grid graph; returns (L~ scipy, lap tuple for the oracle)."""
+    c = case(load_golden("golden_E.npz"))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    return Lt, (c["Lt_rowptr"], c["Lt_col"], c["Lt_val"].astype(np.float64)), M
+
+
+def make_cell(Lt, feat_in, H, K, gates, dev, seed):
+    """A cell on L~ directly (lmax=2 rescale happens in plan_for, so hand it
+    the plan of L~ by constructing from L = L~ + I: rescale_L(L, 2) = L~)."""
+    from cnn_graph_amd.gconv_lstm import GConvLSTMCell
+    L = (Lt + scipy.sparse.identity(Lt.shape[0], dtype=np.float32, format="csr")).tocsr()
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    cell = GConvLSTMCell(H, laplacian=L, lmax=2, K=K, feat_in=feat_in, gates=gates, device=dev,
+                         generator=g)
+    return cell, L
+
+
+def params_np(cell):
+    return [cell.Wx.detach().cpu().numpy().astype(np.float64),
+            cell.Wh.detach().cpu().numpy().astype(np.float64),
+            cell.b.detach().cpu().numpy().astype(np.float64)]
+
+
+def oracle_lap(cell, L):
+    """The L~ the plan actually holds (rescale_L of the cell's L)."""
+    rp, ci, v = cell.plan.rowptr, cell.plan.col, cell.plan.val
+    return (rp, ci, v.astype(np.float64))
+
+
+@pytest.mark.parametrize("gates", ["reference", "standard"])
+def test_pointwise_cell_kernels_vs_numpy(dev, gates):
+    from cnn_graph_amd import ops
+    rng = np.random.default_rng(3)
+    R, H = 1000, 24
+    gx = rng.standard_normal((R, 4 * H)) * 0.5
+    gh = rng.standard_normal((R, 4 * H)) * 0.5
+    b = rng.standard_normal(4 * H) * 0.2
+    c = rng.standard_normal((R, H))
+    dh, dh2, dc = (rng.standard_normal((R, H)) for _ in range(3))
+    gx32, gh32, b32, c32 = (a.astype(np.float32).astype(np.float64) for a in (gx, gh, b, c))
+    c_out, h_out, act = ops.lstm_cell_forward(t(gx, dev), t(gh, dev), t(b, dev), t(c, dev), H, gates)
+    dpre, dcp = ops.lstm_cell_backward(t(dh, dev), t(dh2, dev), t(dc, dev), act, t(c, dev), c_out, H,
+                                       gates)
+    torch.cuda.synchronize()
+    # the kernel's inputs are fp32 and so is its pre-activation sum; tan / tanh
+    # / sigmoid and everything after are checked against float64 from there
+    a = ((gx.astype(np.float32) + gh.astype(np.float32)) + b.astype(np.float32)).astype(np.float64)
+    sig = lambda v: 1 / (1 + np.exp(-v))  # noqa: E731
+    z = np.tan(a[:, :H]) if gates == "reference" else np.tanh(a[:, :H])
+    i, f = sig(a[:, H:2 * H]), sig(a[:, 2 * H:3 * H])
+    o = np.tanh(a[:, 3 * H:]) if gates == "reference" else sig(a[:, 3 * H:])
+    cn = f * c32 + i * z
+    hn = o * np.tanh(cn)
+    assert O.normwise_err(c_out.cpu().numpy(), cn) < TOL
+    assert O.normwise_err(h_out.cpu().numpy(), hn) < TOL
+    assert O.normwise_err(act.cpu().numpy(), np.concatenate([z, i, f, o], 1)) < TOL
+    dh_t = dh.astype(np.float32).astype(np.float64) + dh2.astype(np.float32).astype(np.float64)
+    tc = np.tanh(cn)
+    dcn = dh_t * o * (1 - tc ** 2) + dc.astype(np.float32)
+    d_o = dh_t * tc
+    daz = dcn * i * ((1 + z * z) if gates == "reference" else (1 - z * z))
+    dao = d_o * ((1 - o * o) if gates == "reference" else o * (1 - o))
+    ref = np.concatenate([daz, dcn * z * i * (1 - i), dcn * c32 * f * (1 - f), dao], 1)
+    assert O.normwise_err(dpre.cpu().numpy(), ref) < TOL
+    assert O.normwise_err(dcp.cpu().numpy(), dcn * f) < TOL
+
+
+def test_weight_and_bias_grad_accumulate(dev):
+    from cnn_graph_amd import ops
+    rng = np.random.default_rng(5)
+    R, FK, Fo = 70000, 96, 128
+    A = rng.standard_normal((R, FK)).astype(np.float32)
+    D = rng.standard_normal((R, Fo)).astype(np.float32)
+    W0 = rng.standard_normal((FK, Fo)).astype(np.float32)
+    out = t(W0, dev)
+    ops.weight_grad(t(A, dev), t(D, dev), out=out, accumulate=True)
+    db = ops.bias_grad(t(D, dev))
+    torch.cuda.synchronize()
+    ref = W0.astype(np.float64) + A.astype(np.float64).T @ D.astype(np.float64)
+    assert O.normwise_err(out.cpu().numpy(), ref) < TOL
+    assert O.normwise_err(db.cpu().numpy(), D.astype(np.float64).sum(0)) < TOL
+    # bitwise reproducible (fixed-order reductions)
+    again = ops.weight_grad(t(A, dev), t(D, dev))
+    again2 = ops.weight_grad(t(A, dev), t(D, dev))
+    assert torch.equal(again, again2)
+
+
+@pytest.mark.parametrize("gates", ["reference", "standard"])
+def test_cell_step_autograd_vs_oracle(dev, gates):
+    """GConvLSTMCell.__call__ with a non-zero state, gradients by autograd."""
+    Lt, _, M = graph_E()
+    N, Fin, H, K = 3, 2, 8, 3
+    cell, L = make_cell(Lt, Fin, H, K, gates, dev, seed=11)
+    lap = oracle_lap(cell, L)
+    rng = np.random.default_rng(2)
+    x, c0, h0 = rng.standard_normal((N, M, Fin)), rng.standard_normal((N, M, H)) * 0.5, \
+        rng.standard_normal((N, M, H)) * 0.5
+    gh, gc = rng.standard_normal((N, M, H)), rng.standard_normal((N, M, H))
+    xt, ct, ht = (t(a, dev).requires_grad_() for a in (x, c0, h0))
+    new_h, (new_c, new_h2) = cell(xt, (ct, ht))
+    assert new_h2 is new_h
+    loss = (new_h * t(gh, dev)).sum() + (new_c * t(gc, dev)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    p = params_np(cell)
+    f32 = lambda a: a.astype(np.float32).astype(np.float64)  # noqa: E731
+    cn, hn, cache = LO.cell_forward(f32(x), f32(c0), f32(h0), *p, lap, K, H, gates)
+    dx, dc, dh, dWx, dWh, db, _ = LO.cell_backward(f32(gh), f32(gc), cache, p[0], p[1], lap, K, H, gates)
+    assert O.normwise_err(new_c.detach().cpu().numpy(), cn) < TOL
+    assert O.normwise_err(new_h.detach().cpu().numpy(), hn) < TOL
+    for name, got, ref in (("dx", xt.grad, dx), ("dc", ct.grad, dc), ("dh", ht.grad, dh),
+                           ("dWx", cell.Wx.grad, dWx), ("dWh", cell.Wh.grad, dWh), ("db", cell.b.grad, db)):
+        err = O.normwise_err(got.cpu().numpy(), ref)
+        assert err < TOL, (name, err)
+
+
+@pytest.mark.parametrize("zero_init", [True, False])
+def test_two_layer_static_rnn_vs_oracle(dev, zero_init):
+    """static_rnn(MultiRNNCell([cell1, cell2])) (lib/gconv_lstm.py:609-627),
+    T=4, zero or given initial state, full BPTT."""
+    from cnn_graph_amd.gconv_lstm import static_rnn
+    Lt, _, M = graph_E()
+    T, N, Fin, H, K = 4, 2, 2, 8, 3
+    cell1, L = make_cell(Lt, Fin, H, K, "reference", dev, seed=21)
+    cell2, _ = make_cell(Lt, H, H, K, "reference", dev, seed=22)
+    lap = oracle_lap(cell1, L)
+    rng = np.random.default_rng(4)
+    xs = rng.standard_normal((T, N, M, Fin))
+    gh = rng.standard_normal((T, N, M, H))
+    init = None
+    inits_np = [(None, None), (None, None)]
+    if not zero_init:
+        st = [rng.standard_normal((N, M, H)) * 0.5 for _ in range(4)]
+        inits_np = [(st[0], st[1]), (st[2], st[3])]
+        init = [tuple(t(a, dev).requires_grad_() for a in pair) for pair in inits_np]
+    xt = t(xs, dev).requires_grad_()
+    outs, states = static_rnn([cell1, cell2], list(xt.unbind(0)), init)
+    loss = (torch.stack(outs) * t(gh, dev)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    f32 = lambda a: None if a is None else a.astype(np.float32).astype(np.float64)  # noqa: E731
+    p1, p2 = params_np(cell1), params_np(cell2)
+    h1, c1, ca1 = LO.layer_forward(f32(xs), p1, lap, K, H, f32(inits_np[0][0]), f32(inits_np[0][1]))
+    h2, c2, ca2 = LO.layer_forward(h1, p2, lap, K, H, f32(inits_np[1][0]), f32(inits_np[1][1]))
+    assert O.normwise_err(torch.stack(outs).detach().cpu().numpy(), h2) < TOL
+    assert O.normwise_err(states[0].c.detach().cpu().numpy(), c1[-1]) < TOL
+    dh1, dc02, dh02, dWx2, dWh2, db2 = LO.layer_backward(f32(gh), None, ca2, p2, lap, K, H)
+    dxs, dc01, dh01, dWx1, dWh1, db1 = LO.layer_backward(dh1, None, ca1, p1, lap, K, H)
+    pairs = [("dxs", xt.grad, dxs), ("dWx1", cell1.Wx.grad, dWx1), ("dWh1", cell1.Wh.grad, dWh1),
+             ("db1", cell1.b.grad, db1), ("dWx2", cell2.Wx.grad, dWx2), ("dWh2", cell2.Wh.grad, dWh2),
+             ("db2", cell2.b.grad, db2)]
+    if not zero_init:
+        pairs += [("dc0_1", init[0][0].grad, dc01), ("dh0_1", init[0][1].grad, dh01),
+                  ("dc0_2", init[1][0].grad, dc02), ("dh0_2", init[1][1].grad, dh02)]
+    for name, got, ref in pairs:
+        err = O.normwise_err(got.cpu().numpy(), ref)
+        assert err < TOL, (name, err)
+
+
+def test_config_E_sequence_path_equals_cell_steps(dev):
+    """Config E at full size (M=1024, T=12, K=3, Fin=2, H=32, N=128): the fused
+    sequence path (time-batched x-conv, one dW GEMM for Wh) equals stepping the
+    cell T times under autograd (a size-independent identity), and a small
+    batch of it matches the oracle."""
+    from cnn_graph_amd.gconv_lstm import layer
+    Lt, _, M = graph_E()
+    T, N, Fin, H, K = 12, 128, 2, 32, 3
+    cell, L = make_cell(Lt, Fin, H, K, "reference", dev, seed=31)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    xs = torch.randn((T, N, M, Fin), device=dev, generator=g)
+    gh = torch.randn((T, N, M, H), device=dev, generator=g)
+    xa = xs.clone().requires_grad_()
+    hs, _ = layer(cell, xa)
+    (hs * gh).sum().backward()
+    ga = [p.grad.clone() for p in cell.parameters()] + [xa.grad.clone()]
+    for p in cell.parameters():
+        p.grad = None
+    xb = xs.clone().requires_grad_()
+    c, h = cell.zero_state(N)
+    outs = []
+    for s in range(T):
+        h, (c, _) = cell(xb[s], (c, h))
+        outs.append(h)
+    hb = torch.stack(outs)
+    (hb * gh).sum().backward()
+    gb = [p.grad for p in cell.parameters()] + [xb.grad]
+    torch.cuda.synchronize()
+    assert O.normwise_err(hs.detach().cpu().numpy(), hb.detach().cpu().numpy()) < 1e-6
+    for a, b in zip(ga, gb):
+        assert O.normwise_err(a.cpu().numpy(), b.cpu().numpy()) < 1e-5
+    # oracle on the first 4 samples (the filter is per-sample independent)
+    lap = oracle_lap(cell, L)
+    n = 4
+    f64 = lambda a: a.detach().cpu().numpy().astype(np.float64)  # noqa: E731
+    h_ref, _, _ = LO.layer_forward(f64(xs[:, :n]), params_np(cell), lap, K, H)
+    assert O.normwise_err(f64(hs[:, :n]), h_ref) < TOL
