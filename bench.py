@@ -143,6 +143,11 @@ def main():
     ap.add_argument("--path", default="auto", choices=["auto", "resident", "stream"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "torch"],
+                    help="rccl: cg_allreduce_sum_f32 on the compute stream (default); "
+                         "torch: dist.all_reduce (ProcessGroupNCCL, internal stream + events)")
+    ap.add_argument("--force-allreduce", action="store_true",
+                    help="run the gradient exchange even at N=1 (1-rank RCCL; overhead study)")
     args = ap.parse_args()
 
     rank, world, local = cdist.init()
@@ -173,12 +178,23 @@ def main():
                  W.numel(), ctypes.c_float(1e-3), ctypes.c_float(0.9), ctypes.c_float(0.999),
                  ctypes.c_float(1e-8))
     scale = ctypes.c_float(1.0 / world)
+    exchange = world > 1 or args.force_allreduce
+    comm = None
+    if exchange and args.allreduce == "rccl":
+        comm = cdist.RcclComm(local)
+        ar_fn = _lib.lib().cg_allreduce_sum_f32
+        ar_args = (comm.handle, runner.dW.data_ptr(), runner.dW.numel(), stream)
 
     def step(i):
         runner.forward(x, W, stream=stream)
         runner.backward(dy, W, stream=stream)
-        if world > 1:
-            dist.all_reduce(runner.dW, op=dist.ReduceOp.SUM)
+        if exchange:
+            if comm is not None:
+                st = ar_fn(*ar_args)
+                if st:
+                    _lib.check("cg_allreduce_sum_f32", st)
+            else:
+                dist.all_reduce(runner.dW, op=dist.ReduceOp.SUM)
         st = adam(*adam_args, i + 1, scale, stream)
         if st:
             _lib.check("cg_adam_update", st)
@@ -239,7 +255,8 @@ def main():
         "config": {"workload": "config B: MNIST 8-NN grid coarsened, M=976, nnz=6396, K=25, Fin=1, "
                                "Fout=32, chebyshev5 fwd+bwd + dW all-reduce + Adam",
                    "batch_per_gpu": N, "global_batch": N * world, "M": M, "nnz": plan.nnz, "K": K,
-                   "Fin": Fin, "Fout": Fout, "path": path, "parallelism": f"dp{world}"},
+                   "Fin": Fin, "Fout": Fout, "path": path, "parallelism": f"dp{world}",
+                   "allreduce": (args.allreduce if exchange else None)},
         "roofline": {"bound": "hbm", "kernel": kern[dom]["kernel"],
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4),
@@ -260,6 +277,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(L, fake, K, Fout, seconds=args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -7,10 +7,13 @@ is used for the CPU tests.  Gradient buckets on this path are a few KB
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
 import torch.distributed as dist
+
+from . import _lib
 
 
 def env_rank_world():
@@ -66,3 +69,53 @@ def shard(n_global: int, rank: int, world: int):
     lo = rank * per
     hi = n_global if rank == world - 1 else lo + per
     return lo, hi
+
+
+class RcclComm:
+    """An RCCL communicator of libcheb_mi355 (cg_comm_* in the C ABI) over the
+    ranks of a torch.distributed group: rank 0 creates the unique id, the group
+    broadcasts it, every rank joins.  ``allreduce_sum_`` enqueues ncclAllReduce
+    directly on the caller's HIP stream -- no side stream and no event
+    fork/join around it (what ProcessGroupNCCL adds to every collective), so a
+    step's gradient exchange is one kernel in stream order.  With no process
+    group (single process) it is a 1-rank communicator."""
+
+    def __init__(self, device: int, group=None):
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            _lib.call("cg_comm_unique_id", uid)
+        if self.world > 1:
+            t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
+            if dist.get_backend(group) == "nccl":
+                t = t.cuda(device)
+            dist.broadcast(t, src=0, group=group)
+            uid = ctypes.create_string_buffer(bytes(t.cpu().tolist()), 128)
+        h = ctypes.c_void_p()
+        _lib.call("cg_comm_init", ctypes.byref(h), self.world, self.rank, uid, int(device))
+        self._h = h
+        self._fn = _lib.lib().cg_allreduce_sum_f32
+
+    @property
+    def handle(self):
+        return self._h
+
+    def allreduce_sum_(self, t: torch.Tensor, stream=None):
+        """In-place SUM over ranks of a contiguous fp32 device tensor."""
+        if not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("allreduce_sum_ needs a contiguous fp32 device tensor")
+        s = stream if stream is not None else torch.cuda.current_stream(t.device).cuda_stream
+        _lib.check("cg_allreduce_sum_f32", self._fn(self._h, t.data_ptr(), t.numel(), s))
+        return t
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            _lib.lib().cg_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -241,3 +241,17 @@ def test_bad_shapes_raise(dev):
     big = make_plan(c, "resident")
     with pytest.raises(_lib.CGError):
         ops.cheb_forward(big, torch.zeros((1, c["M"], 4096), device=dev), None, 40)
+
+
+def test_rccl_comm_single_rank_allreduce(dev):
+    """cg_comm_unique_id / cg_comm_init / cg_allreduce_sum_f32 / cg_comm_destroy
+    on a real GPU (1-rank communicator: the sum is the identity)."""
+    from cnn_graph_amd.dist import RcclComm
+    comm = RcclComm(0)
+    assert comm.world == 1
+    a = torch.arange(800, device=dev, dtype=torch.float32) * 0.5
+    ref = a.clone()
+    comm.allreduce_sum_(a)
+    torch.cuda.synchronize()
+    assert torch.equal(a, ref)
+    comm.close()
