@@ -172,6 +172,24 @@ def config_e():
     save("golden_E.npz", **case)
 
 
+def config_c():
+    """20NEWS-like vocabulary graph: 10 000 x 100 Gaussian
+    embeddings (np.random.seed(0)), cosine 16-NN via the reference's
+    distance_sklearn_metrics / adjacency / laplacian -> nnz(L~) = 182 466,
+    max row nnz 32.  Streaming-path sizes (M > 2048)."""
+    np.random.seed(0)
+    X = np.random.normal(0, 1, (10000, 100)).astype(np.float32)
+    dist, idx = graph.distance_sklearn_metrics(X, k=16, metric="cosine")
+    A = graph.adjacency(dist, idx)
+    L = graph.laplacian(A, normalized=True)
+    case = cheb_case(L, N=2, Fin=1, K=5, Fout=8, seed=2022)      # layer 1 (Fin=1)
+    case2 = cheb_case(L, N=1, Fin=3, K=5, Fout=4, seed=2023)     # Fin>1 layout
+    assert int(case["Lt_rowptr"][-1]) == 182466
+    out = {**case, **{f"fin3_{k}": v for k, v in case2.items()
+                      if not k.startswith("Lt_")}}
+    save("golden_C.npz", **out)
+
+
 def misc():
     # (iii) compute_perm known answer, lib/coarsening.py:216-217
     parents = [np.array([4, 1, 1, 2, 2, 3, 0, 0, 3]), np.array([2, 1, 0, 1, 0])]
@@ -195,7 +213,7 @@ def misc():
 
 
 if __name__ == "__main__":
-    config_a()
-    config_b()
-    config_e()
-    misc()
+    # optional argv: the fixtures to (re)generate, e.g. `make_golden.py config_c`
+    todo = sys.argv[1:] or ["config_a", "config_b", "config_e", "config_c", "misc"]
+    for name in todo:
+        globals()[name]()

@@ -159,3 +159,19 @@ def test_maxpool_first_max_rule():
         dx = O.mpool1_backward(dy, arg, M)
         assert np.isclose(dx.sum(), dy.sum(), atol=1e-4)
         assert (dx != 0).sum() <= dy.size
+
+
+@pytest.mark.parametrize("prefix", ["", "fin3_"])
+def test_config_c_oracle_vs_reference(prefix):
+    """Config C (10 000-vertex cosine 16-NN graph built by the reference's
+    lib/graph.py): oracle basis bit-equal to lib/graph.py::chebyshev, outputs
+    vs the float64 truth."""
+    g = load_golden("golden_C.npz")
+    c = case(g, prefix)
+    rp, ci, v = g["Lt_rowptr"], g["Lt_col"], g["Lt_val"]
+    basis, y = O.cheb_forward(c["x"], rp, ci, v, c["W"], c["K"])
+    assert np.array_equal(basis, c["basis"])
+    assert O.normwise_err(y, c["y_ref"]) < 1e-6
+    dx, dW = O.cheb_backward(c["dy"], basis, c["W"], rp, ci, v, c["N"], int(g["M"]), c["Fin"], c["K"])
+    assert O.normwise_err(dx, c["dx_ref"]) < 1e-6
+    assert O.normwise_err(dW, c["dW_ref"]) < 1e-10
