@@ -144,21 +144,34 @@ hipError_t launch_fast_forward(const FastGeom& g, int N, const FastFwdArgs& a, h
 hipError_t launch_fast_backward(const FastGeom& g, int N, const FastBwdArgs& a, hipStream_t s);
 
 // ---- streaming path ----------------------------------------------------------
-hipError_t launch_x_to_cols(const float* x, float* T0, float* basis, int N, int M, int Fin, int K,
-                            hipStream_t s);
-hipError_t launch_spmm_cheb_step(const int* rowptr, const int* col, const float* val,
-                                 const float* Tprev, const float* Tprev2, float* Tout, float* basis,
-                                 int N, int M, int Fin, int K, int k, hipStream_t s);
-hipError_t launch_clenshaw_step(const int* trowptr, const int* tcol, const float* tval,
-                                const float* Gn1, const float* Gn2, float* Gout, const float* dA,
-                                float* dx, int N, int M, int Fin, int K, int k, hipStream_t s);
+// One Chebyshev step over all (sample, row) pairs in the sample-major layout
+// (T_k [N][M][Fin], T_0 = x).  last: also assemble the basis [N*M][Fin*K]
+// from x, slots (T_1..T_{K-2}, N*M*Fin floats apart) and the new T_{K-1}.
+// rperm: row visiting order (NULL = natural).
+hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val, const int* rperm,
+                            const float* Tp, const float* Tpp, float* Tout, const float* x,
+                            const float* slots, float* basis, int N, int M, int Fin, int K, int k,
+                            bool last, hipStream_t s);
+// Reverse step G_k = D_k + c L~^T G_{k+1} - G_{k+2} (sample-major; k = 0 -> dx).
+hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tval, const int* rperm,
+                           const float* Gn1, const float* Gn2, float* Gout, const float* Dk, int N,
+                           int M, int Fin, int K, int k, hipStream_t s);
 // C[Mg x Ng] (+)= op(A)[Mg x Kg] * op(B)[Kg x Ng]; fp32 in/out on MFMA f32.
 // trans_a: A stored [Kg][lda] (A^T row-major); trans_b: B stored [Ng][ldb].
 // splits > 1: the K range is cut into `splits` slices, slice s writes
 // C + s*Mg*ldc (a partial slab, reduced later by launch_reduce_slabs).
+// Skinny row GEMM on MFMA (persistent, B staged in LDS): for p < planes,
+// C[p*c_plane + r*ldc + j] = sum_k A[r*lda + k] * B[p*bs_p + k*bs_k + j*bs_j],
+// r < R, k < Kc, j < Nc.  rowgemm_ok says whether the shape is supported.
+bool rowgemm_ok(int Kc, int lda, int Nc);
+hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
+                          int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
+                          int64_t c_plane, hipStream_t s);
+// remapK > 0: write C in the k-major [remapK][Mg][Ng/remapK] layout instead
+// (column fin*K + k -> plane k), splits must be 1.
 hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, const float* A,
                            int lda, const float* B, int ldb, float* C, int ldc, int splits,
-                           hipStream_t s);
+                           hipStream_t s, int remapK = 0);
 // dW = basis^T dy as per-chunk partial slabs ([dw_chunks(R)][FinK][Fout]),
 // R = N*M basis rows; reduce with launch_reduce_slabs.
 int dw_chunks(int64_t R);

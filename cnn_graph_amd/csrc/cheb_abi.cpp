@@ -31,6 +31,11 @@ struct cg_plan {
   int* trowptr = nullptr;
   int* tcol = nullptr;
   float* tval = nullptr;
+  // degree-sorted row orders of L~ / L~^T (longest rows first), used by the
+  // streaming steps on skewed (power-law) graphs so a wave's rows have similar
+  // lengths; null when the row lengths are near-uniform
+  int* rperm = nullptr;
+  int* trperm = nullptr;
   hipStream_t side = nullptr;  // dW kernel runs here, overlapped with the dx recurrence
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // thread-slot images of L~ and L~^T for the resident kernels (M <= 2048)
@@ -244,7 +249,7 @@ int upload(T** dst, const T* src, size_t count) {
 
 void free_plan(cg_plan* p) {
   if (!p) return;
-  void* ptrs[] = {p->rowptr, p->col, p->val, p->trowptr, p->tcol, p->tval};
+  void* ptrs[] = {p->rowptr, p->col, p->val, p->trowptr, p->tcol, p->tval, p->rperm, p->trperm};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (p->slots.buf) (void)hipFree(p->slots.buf);
@@ -315,8 +320,9 @@ int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool bac
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 struct StreamWs {
-  size_t ring;  // 3 * M * B floats
-  size_t dA;    // N*M*FinK floats
+  size_t slots;  // forward: T_1 .. T_{K-2}, (K-2) * N*M*Fin floats
+  size_t ring;   // backward: G ring, 3 * N*M*Fin floats
+  size_t dA;     // backward: dBasis, N*M*FinK floats (k-major)
 };
 
 StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout) {
@@ -324,6 +330,7 @@ StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t 
   const int64_t B = int64_t(N) * Fin;
   const int64_t FinK = int64_t(Fin) * K;
   const int64_t NM = int64_t(N) * p->M;
+  w.slots = al256(size_t(K > 2 ? K - 2 : 0) * size_t(p->M) * size_t(B) * 4);
   w.ring = al256(size_t(3) * size_t(p->M) * size_t(B) * 4);
   w.dA = al256(size_t(NM) * size_t(FinK) * 4);
   (void)Fout;
@@ -346,7 +353,7 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
   if ((rc = choose_path(p, Fin, K, Fout, true, &pb))) return rc;
   const StreamWs w = stream_ws(p, N, Fin, K, Fout);
   const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, N, Fin * K, Fout);
-  *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.ring;
+  *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.slots;
   *bwd = slabs + ((pb == CG_PATH_RESIDENT) ? 0 : (w.ring + w.dA));
   return CG_OK;
 }
@@ -468,6 +475,19 @@ int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz, const int
   if (!rc) rc = upload(&p->trowptr, trp.data(), trp.size());
   if (!rc) rc = upload(&p->tcol, tci.data(), tci.size());
   if (!rc) rc = upload(&p->tval, tv.data(), tv.size());
+  if (!rc && nnz > 0 && p->max_row_nnz > 2 * (nnz / M) + 8) {
+    auto order = [M](const int32_t* rp) {
+      std::vector<int32_t> o(size_t(M), 0);
+      for (int32_t r = 0; r < M; ++r) o[size_t(r)] = r;
+      std::stable_sort(o.begin(), o.end(), [rp](int32_t a, int32_t b) {
+        return rp[a + 1] - rp[a] > rp[b + 1] - rp[b];
+      });
+      return o;
+    };
+    const std::vector<int32_t> o = order(rowptr), ot = order(trp.data());
+    rc = upload(&p->rperm, o.data(), o.size());
+    if (!rc) rc = upload(&p->trperm, ot.data(), ot.size());
+  }
   if (!rc && nnz > 0) rc = build_slots(&p->slots, M, rowptr, col, val);
   if (!rc && nnz > 0) rc = build_slots(&p->tslots, M, trp.data(), tci.data(), tv.data());
   if (!rc && nnz > 0) rc = build_fast_image(&p->fast, M, rowptr, col, val);
@@ -565,19 +585,32 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
   // streaming path
   if (!basis) return fail(CG_ERR_ARG, "streaming path needs a basis buffer (the GEMM reads it)");
   const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
-  if (!workspace || ws_bytes < w.ring)
-    return fail(CG_ERR_ARG, "forward workspace too small: %zu < %zu", ws_bytes, w.ring);
-  float* ring = static_cast<float*>(workspace);
+  if (w.slots && (!workspace || ws_bytes < w.slots))
+    return fail(CG_ERR_ARG, "forward workspace too small: %zu < %zu", ws_bytes, w.slots);
+  float* slots = static_cast<float*>(workspace);
   const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
-  auto T = [&](int k) { return ring + size_t(k % 3) * slot; };
-  CG_HIP(cg::launch_x_to_cols(x, T(0), basis, N, M, Fin, K, s));
-  for (int k = 1; k < K; ++k)
-    CG_HIP(cg::launch_spmm_cheb_step(plan->rowptr, plan->col, plan->val, T(k - 1),
-                                     k >= 2 ? T(k - 2) : nullptr, (k < K - 1) ? T(k) : nullptr,
-                                     basis, N, M, Fin, K, k, s));
-  if (y)
-    CG_HIP(cg::launch_gemm_f32(false, false, N * M, Fout, Fin * K, basis, Fin * K, W, Fout, y,
-                               Fout, 1, s));
+  // sample-major steps: T_0 = x, T_j (1 <= j <= K-2) in slots[j-1], the last
+  // step writes the whole basis (lib/graph_conv.py:159-172)
+  const int* rperm = (Fin >= 16) ? plan->rperm : nullptr;
+  auto T = [&](int k) -> const float* { return k == 0 ? x : slots + size_t(k - 1) * slot; };
+  if (K == 1)
+    CG_HIP(hipMemcpyAsync(basis, x, slot * sizeof(float), hipMemcpyDeviceToDevice, s));
+  for (int k = 1; k < K; ++k) {
+    const bool last = (k == K - 1);
+    CG_HIP(cg::launch_cheb_step(plan->rowptr, plan->col, plan->val, rperm, T(k - 1),
+                                k >= 2 ? T(k - 2) : nullptr,
+                                last ? nullptr : slots + size_t(k - 1) * slot, x, slots, basis, N,
+                                M, Fin, K, k, last, s));
+  }
+  if (y) {
+    const int FinK = Fin * K;
+    if (cg::rowgemm_ok(FinK, FinK, Fout))
+      CG_HIP(cg::launch_rowgemm(basis, int64_t(N) * M, FinK, FinK, W, Fout, 1, 0, 1, Fout, y, Fout,
+                                0, s));
+    else
+      CG_HIP(cg::launch_gemm_f32(false, false, N * M, Fout, FinK, basis, FinK, W, Fout, y, Fout, 1,
+                                 s));
+  }
   return ok();
 }
 
@@ -659,13 +692,21 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
       float* ring = reinterpret_cast<float*>(rest);
       float* dA = reinterpret_cast<float*>(rest + w.ring);
       const int NM = N * M;
-      // dBasis = dy W^T, then the reverse recurrence one launch per step
-      CG_HIP(cg::launch_gemm_f32(false, true, NM, FinK, Fout, dy, Fout, W, Fout, dA, FinK, 1, s));
+      // dBasis = dy W^T written k-major ([K][N*M][Fin]), then the reverse
+      // recurrence one launch per step in the sample-major layout
       const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
+      if (cg::rowgemm_ok(Fout, Fout, Fin))  // plane k: dA_k[r][fin] = sum_f dy[r][f] W[fin*K+k][f]
+        CG_HIP(cg::launch_rowgemm(dy, NM, Fout, Fout, W, 1, int64_t(K) * Fout, Fout, K, Fin, dA, Fin,
+                                  int64_t(slot), s));
+      else
+        CG_HIP(cg::launch_gemm_f32(false, true, NM, FinK, Fout, dy, Fout, W, Fout, dA, FinK, 1, s, K));
+      const int* rperm = (Fin >= 16) ? plan->trperm : nullptr;
       auto G = [&](int k) { return ring + size_t(k % 3) * slot; };
       for (int k = K - 1; k >= 0; --k)
-        CG_HIP(cg::launch_clenshaw_step(plan->trowptr, plan->tcol, plan->tval, G(k + 1), G(k + 2),
-                                        G(k), dA, dx, N, M, Fin, K, k, s));
+        CG_HIP(cg::launch_clenshaw(plan->trowptr, plan->tcol, plan->tval, rperm,
+                                   (k + 1 <= K - 1) ? G(k + 1) : nullptr,
+                                   (k + 2 <= K - 1) ? G(k + 2) : nullptr, k == 0 ? dx : G(k),
+                                   dA + size_t(k) * slot, N, M, Fin, K, k, s));
     }
   }
   if (!dW) return ok();

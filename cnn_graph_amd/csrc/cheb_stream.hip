@@ -28,105 +28,357 @@ inline int grid_for(int64_t total, int block) {
   return int(g);
 }
 
-__global__ __launch_bounds__(256) void k_x_to_cols(const float* __restrict__ x,
-                                                   float* __restrict__ T0,
-                                                   float* __restrict__ basis, int N, int M,
-                                                   int Fin, int K) {
-  const int64_t B = int64_t(N) * Fin;
-  const int64_t total = int64_t(M) * B;
-  const int64_t FinK = int64_t(Fin) * K;
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t m = i / B, b = i - m * B;
-    const int64_t n = b / Fin, fin = b - n * Fin;
-    const float v = x[(n * M + m) * Fin + fin];
-    T0[i] = v;
-    if (basis) basis[(n * M + m) * FinK + fin * K] = v;
-  }
-}
+// ---- Chebyshev steps in the sample-major layout ---------------------------------
+// T_k is stored like x: [N][M][Fin] (T_0 IS x, no transpose).  A work item is
+// one (sample n, vertex row r): LPR lanes own its Fin columns (VEC floats per
+// lane), a wave holds 64/LPR rows.  Gathers of T_{k-1}[n][c][:] read Fin*4
+// contiguous bytes of the SAME sample, so a sample's slab (M*Fin*4 bytes) is
+// the gathered working set; blocks are mapped so that each XCD works through
+// its own samples (n = xcd, xcd+8, ...) and that slab stays in its L2.
+// The last step assembles the basis row (n, r) = [fin][k] (lib/graph_conv.py:172)
+// from the own-row T_0..T_{K-2} and the fresh T_{K-1}: every basis byte is
+// written once, by one lane, contiguously.
+struct StepGeom {
+  int lpr;      // lanes per row
+  int rpw;      // rows per wave (64 / lpr)
+  int rb;       // row blocks (of 4 waves) per sample
+  int xcd_map;  // 1: sample-per-XCD block mapping (N % 8 == 0)
+};
 
-// (n*M + r)*Fin*K + fin*K for dense column b = n*Fin + fin
-__device__ __forceinline__ int64_t row_base(int64_t r, int64_t b, int M, int Fin, int K) {
-  const int64_t n = b / Fin, fin = b - n * Fin;
-  return (n * M + r) * (int64_t(Fin) * K) + fin * K;
-}
-
-template <bool VEC4>
-__global__ __launch_bounds__(256) void k_spmm_cheb(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
-    const float* __restrict__ Tprev, const float* __restrict__ Tprev2, float* __restrict__ Tout,
-    float* __restrict__ basis, int N, int M, int Fin, int K, int k) {
-#pragma clang fp contract(off)
-  const int64_t B = int64_t(N) * Fin;
-  const int r = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + int(threadIdx.x >> 6));
-  if (r >= M) return;
-  const int lane = threadIdx.x & 63;
-  const int j0 = rowptr[r], j1 = rowptr[r + 1];
-  if (VEC4) {
-    for (int64_t b = int64_t(lane) * 4; b < B; b += 256) {
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int j = j0; j < j1; ++j) {
-        const float v = val[j];
-        const float4 t = *reinterpret_cast<const float4*>(Tprev + int64_t(col[j]) * B + b);
-        a.x = a.x + v * t.x;
-        a.y = a.y + v * t.y;
-        a.z = a.z + v * t.z;
-        a.w = a.w + v * t.w;
-      }
-      float4 o = a;
-      if (k >= 2) {
-        const float4 p = *reinterpret_cast<const float4*>(Tprev2 + int64_t(r) * B + b);
-        o.x = 2.f * a.x - p.x;
-        o.y = 2.f * a.y - p.y;
-        o.z = 2.f * a.z - p.z;
-        o.w = 2.f * a.w - p.w;
-      }
-      if (Tout) *reinterpret_cast<float4*>(Tout + int64_t(r) * B + b) = o;
-      if (basis) {
-        basis[row_base(r, b + 0, M, Fin, K) + k] = o.x;
-        basis[row_base(r, b + 1, M, Fin, K) + k] = o.y;
-        basis[row_base(r, b + 2, M, Fin, K) + k] = o.z;
-        basis[row_base(r, b + 3, M, Fin, K) + k] = o.w;
-      }
-    }
+__device__ __forceinline__ void block_coords(const StepGeom g, int* n, int* rb) {
+  const int i = blockIdx.x;
+  if (g.xcd_map) {
+    const int x = i & 7, q = i >> 3;
+    *n = x + 8 * (q / g.rb);
+    *rb = q % g.rb;
   } else {
-    for (int64_t b = lane; b < B; b += 64) {
-      float a = 0.f;
-      for (int j = j0; j < j1; ++j) a = a + val[j] * Tprev[int64_t(col[j]) * B + b];
-      const float o = (k >= 2) ? (2.f * a - Tprev2[int64_t(r) * B + b]) : a;
-      if (Tout) Tout[int64_t(r) * B + b] = o;
-      if (basis) basis[row_base(r, b, M, Fin, K) + k] = o;
+    *n = i / g.rb;
+    *rb = i % g.rb;
+  }
+}
+
+template <int VEC>
+struct Vec;
+template <>
+struct Vec<1> {
+  typedef float T;
+  static __device__ __forceinline__ T ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, T v) { *p = v; }
+  static __device__ __forceinline__ T zero() { return 0.f; }
+  static __device__ __forceinline__ float get(const T& v, int) { return v; }
+  static __device__ __forceinline__ T fma_seq(T a, float w, T t) {
+#pragma clang fp contract(off)
+    return a + w * t;
+  }
+  static __device__ __forceinline__ T two_minus(T a, T p) {
+#pragma clang fp contract(off)
+    return 2.f * a - p;
+  }
+  static __device__ __forceinline__ T add_c_sub(T d, float c, T a) {
+#pragma clang fp contract(off)
+    return d + c * a;
+  }
+  static __device__ __forceinline__ T sub(T a, T b) { return a - b; }
+};
+template <>
+struct Vec<4> {
+  typedef float4 T;
+  static __device__ __forceinline__ T ld(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  static __device__ __forceinline__ void st(float* p, T v) { *reinterpret_cast<float4*>(p) = v; }
+  static __device__ __forceinline__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ float get(const T& v, int i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+  }
+  static __device__ __forceinline__ T fma_seq(T a, float w, T t) {
+#pragma clang fp contract(off)
+    return make_float4(a.x + w * t.x, a.y + w * t.y, a.z + w * t.z, a.w + w * t.w);
+  }
+  static __device__ __forceinline__ T two_minus(T a, T p) {
+#pragma clang fp contract(off)
+    return make_float4(2.f * a.x - p.x, 2.f * a.y - p.y, 2.f * a.z - p.z, 2.f * a.w - p.w);
+  }
+  static __device__ __forceinline__ T add_c_sub(T d, float c, T a) {
+#pragma clang fp contract(off)
+    return make_float4(d.x + c * a.x, d.y + c * a.y, d.z + c * a.z, d.w + c * a.w);
+  }
+  static __device__ __forceinline__ T sub(T a, T b) {
+#pragma clang fp contract(off)
+    return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+  }
+};
+
+// sum_{j in row r, CSR order} val[j] * S[col[j]*Fin + f0 .. +VEC), sequential
+// from +0 with one rounding per product and per add (the order of scipy
+// csr_matvecs / TF's SparseTensorDenseMatMul).  Four entries' loads are issued
+// before their (in-order) accumulation.
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T row_spmm(const int* __restrict__ col,
+                                                         const float* __restrict__ val, int j0,
+                                                         int j1, const float* __restrict__ S,
+                                                         int Fin, int f0) {
+#pragma clang fp contract(off)
+  typedef Vec<VEC> V;
+  typename V::T acc = V::zero();
+  int j = j0;
+  for (; j + 4 <= j1; j += 4) {
+    const int c0 = col[j], c1 = col[j + 1], c2 = col[j + 2], c3 = col[j + 3];
+    const float v0 = val[j], v1 = val[j + 1], v2 = val[j + 2], v3 = val[j + 3];
+    const typename V::T t0 = V::ld(S + int64_t(c0) * Fin + f0);
+    const typename V::T t1 = V::ld(S + int64_t(c1) * Fin + f0);
+    const typename V::T t2 = V::ld(S + int64_t(c2) * Fin + f0);
+    const typename V::T t3 = V::ld(S + int64_t(c3) * Fin + f0);
+    acc = V::fma_seq(acc, v0, t0);
+    acc = V::fma_seq(acc, v1, t1);
+    acc = V::fma_seq(acc, v2, t2);
+    acc = V::fma_seq(acc, v3, t3);
+  }
+  for (; j < j1; ++j) acc = V::fma_seq(acc, val[j], V::ld(S + int64_t(col[j]) * Fin + f0));
+  return acc;
+}
+
+struct ChebStepArgs {
+  const int* rowptr;
+  const int* col;
+  const float* val;
+  const int* rperm;   // row visiting order (degree-sorted) or NULL
+  const float* Tp;    // T_{k-1}
+  const float* Tpp;   // T_{k-2} (k >= 2)
+  float* Tout;        // T_k (not last step)
+  const float* x;     // T_0 (last step)
+  const float* slots; // T_1 .. T_{K-2}, slot_elems apart (last step)
+  int64_t slot_elems; // N*M*Fin
+  float* basis;       // (last step)
+  int M, Fin, K, k;
+};
+
+template <int VEC, bool LAST>
+__global__ __launch_bounds__(256) void k_cheb_step(ChebStepArgs a, StepGeom g) {
+#pragma clang fp contract(off)
+  typedef Vec<VEC> V;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int n, rb;
+  block_coords(g, &n, &rb);
+  const int rsub = lane / g.lpr, lc = lane - rsub * g.lpr;
+  if (rsub >= g.rpw) return;
+  const int ri = (rb * 4 + wave) * g.rpw + rsub;
+  if (ri >= a.M) return;
+  const int r = a.rperm ? a.rperm[ri] : ri;
+  const int j0 = a.rowptr[r], j1 = a.rowptr[r + 1];
+  const int64_t sbase = int64_t(n) * a.M * a.Fin;
+  const int64_t rbase = sbase + int64_t(r) * a.Fin;
+  const float* S = a.Tp + sbase;
+  for (int f0 = lc * VEC; f0 < a.Fin; f0 += g.lpr * VEC) {
+    const typename V::T acc = row_spmm<VEC>(a.col, a.val, j0, j1, S, a.Fin, f0);
+    const typename V::T o = (a.k >= 2) ? V::two_minus(acc, V::ld(a.Tpp + rbase + f0)) : acc;
+    if (!LAST) {
+      V::st(a.Tout + rbase + f0, o);
+    } else {
+      float* brow = a.basis + (int64_t(n) * a.M + r) * int64_t(a.Fin) * a.K;
+      for (int kk = 0; kk < a.K - 1; ++kk) {
+        const float* Tk = (kk == 0) ? a.x : a.slots + int64_t(kk - 1) * a.slot_elems;
+        const typename V::T tv = V::ld(Tk + rbase + f0);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) brow[(f0 + v) * a.K + kk] = V::get(tv, v);
+      }
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) brow[(f0 + v) * a.K + a.K - 1] = V::get(o, v);
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_clenshaw(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
-    const float* __restrict__ Gn1, const float* __restrict__ Gn2, float* __restrict__ Gout,
-    const float* __restrict__ dA, float* __restrict__ dx, int N, int M, int Fin, int K, int k) {
+// Last forward step with the basis assembly staged through LDS: each wave
+// writes its rows' [fin][k] basis rows into LDS, then stores them with
+// coalesced 4-B lane stores (consecutive rows are one contiguous span in the
+// natural row order; with rperm each row's Fin*K floats are).
+template <int VEC>
+__global__ __launch_bounds__(256) void k_cheb_last(ChebStepArgs a, StepGeom g) {
 #pragma clang fp contract(off)
-  const int64_t B = int64_t(N) * Fin;
-  const int r = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + int(threadIdx.x >> 6));
-  if (r >= M) return;
-  const int lane = threadIdx.x & 63;
-  const int j0 = rowptr[r], j1 = rowptr[r + 1];
-  const bool has1 = (k + 1) <= (K - 1), has2 = (k + 2) <= (K - 1);
-  const float c = (k >= 1) ? 2.f : 1.f;
-  for (int64_t b = lane; b < B; b += 64) {
-    float a = 0.f;
-    if (has1)
-      for (int j = j0; j < j1; ++j) a = a + val[j] * Gn1[int64_t(col[j]) * B + b];
-    float g = dA[row_base(r, b, M, Fin, K) + k] + c * a;
-    if (has2) g = g - Gn2[int64_t(r) * B + b];
-    if (k == 0) {
-      if (dx) {
-        const int64_t n = b / Fin, fin = b - n * Fin;
-        dx[(n * M + r) * Fin + fin] = g;
+  typedef Vec<VEC> V;
+  extern __shared__ float stage[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int n, rb;
+  block_coords(g, &n, &rb);
+  const int FinK = a.Fin * a.K;
+  float* ws = stage + wave * g.rpw * FinK;
+  const int rsub = lane / g.lpr, lc = lane - rsub * g.lpr;
+  const int ri0 = (rb * 4 + wave) * g.rpw;
+  const int ri = ri0 + rsub;
+  if (rsub < g.rpw && ri < a.M) {
+    const int r = a.rperm ? a.rperm[ri] : ri;
+    const int j0 = a.rowptr[r], j1 = a.rowptr[r + 1];
+    const int64_t sbase = int64_t(n) * a.M * a.Fin;
+    const int64_t rbase = sbase + int64_t(r) * a.Fin;
+    float* srow = ws + rsub * FinK;
+    for (int f0 = lc * VEC; f0 < a.Fin; f0 += g.lpr * VEC) {
+      const typename V::T acc = row_spmm<VEC>(a.col, a.val, j0, j1, a.Tp + sbase, a.Fin, f0);
+      const typename V::T o = (a.k >= 2) ? V::two_minus(acc, V::ld(a.Tpp + rbase + f0)) : acc;
+      for (int kk = 0; kk < a.K - 1; ++kk) {
+        const float* Tk = (kk == 0) ? a.x : a.slots + int64_t(kk - 1) * a.slot_elems;
+        const typename V::T tv = V::ld(Tk + rbase + f0);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) srow[(f0 + v) * a.K + kk] = V::get(tv, v);
       }
-    } else {
-      Gout[int64_t(r) * B + b] = g;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) srow[(f0 + v) * a.K + a.K - 1] = V::get(o, v);
     }
   }
+  __syncthreads();
+  if (ri0 >= a.M) return;
+  const int nrows = (a.M - ri0 < g.rpw) ? a.M - ri0 : g.rpw;
+  if (!a.rperm) {
+    float* dst = a.basis + (int64_t(n) * a.M + ri0) * FinK;
+    const int count = nrows * FinK;
+    for (int e = lane; e < count; e += 64) dst[e] = ws[e];
+  } else {
+    for (int q = 0; q < nrows; ++q) {
+      float* dst = a.basis + (int64_t(n) * a.M + a.rperm[ri0 + q]) * FinK;
+      for (int e = lane; e < FinK; e += 64) dst[e] = ws[q * FinK + e];
+    }
+  }
+}
+
+// ---- skinny row GEMM on MFMA --------------------------------------------------------
+// C[p][r][j] = sum_k A[r][k] * B_p[k][j] for R (huge) rows, Kc, Nc <= 256:
+// the contraction y = basis W (lib/graph_conv.py:175), and dBasis = dy W^T
+// written one k-plane at a time (p = k, B_p[f][fin] = W[fin*K + k][f]) so the
+// streaming backward reads D_k contiguously.  B_p is staged once per block in
+// LDS; blocks are persistent over 128-row tiles (a 32-row tile per wave).
+// MFMA 32x32x2 f32 with the k index split in halves: lane (i, h) feeds
+// A[r0+i][h*KC2 + s] at step s, read straight from HBM as contiguous
+// 64-byte chunks of its half-row (no LDS for A), B[h*KC2 + s][j] from LDS.
+struct RowGemmArgs {
+  const float* A;
+  int64_t R;
+  int Kc, lda, KC2;        // KC2 = half of Kc rounded up to a multiple of 16
+  const float* B;          // B_p[k][j] = B[p*bs_p + k*bs_k + j*bs_j]
+  int64_t bs_k, bs_j, bs_p;
+  int Nc;
+  float* C;
+  int ldc;
+  int64_t c_plane;
+};
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
+  extern __shared__ float Bs[];  // [2*KC2][NT*32]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int p = blockIdx.y;
+  const int KP = 2 * a.KC2, NP = NT * 32;
+  for (int e = tid; e < KP * NP; e += 256) {
+    const int kk = e / NP, j = e - kk * NP;
+    // row kk of the padded operand: half 0 holds k < KC2, half 1 holds KC2 + (kk - KC2)
+    const int k = kk;
+    float v = 0.f;
+    if (k < a.Kc && j < a.Nc) v = a.B[p * a.bs_p + int64_t(k) * a.bs_k + int64_t(j) * a.bs_j];
+    Bs[e] = v;
+  }
+  __syncthreads();
+  float* C = a.C + p * a.c_plane;
+  const int64_t ntiles = (a.R + 127) / 128;
+  const int kbeg = h * a.KC2;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * 128 + wave * 32;
+    if (r0 >= a.R) continue;
+    const int64_t row = (r0 + i < a.R) ? r0 + i : a.R - 1;
+    const float* arow = a.A + row * a.lda;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+    for (int c0 = 0; c0 < a.KC2; c0 += 16) {
+      float av[16];
+      const int k0 = kbeg + c0;
+      if (k0 + 16 <= a.Kc && (kbeg + c0 + 16 <= kbeg + a.KC2)) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(arow + k0 + 4 * q);
+          av[4 * q] = v.x;
+          av[4 * q + 1] = v.y;
+          av[4 * q + 2] = v.z;
+          av[4 * q + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) av[q] = (k0 + q < a.Kc) ? arow[k0 + q] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float* brow = Bs + (kbeg + c0 + q) * NP + i;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], brow[t * 32], acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = t * 32 + i;
+      if (col >= a.Nc) continue;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (rr < a.R) C[rr * a.ldc + col] = acc[t][q];
+      }
+    }
+  }
+}
+
+// Reverse (Clenshaw) step over L~^T in the sample-major layout:
+//   G_k = D_k + c * (L~^T G_{k+1}) - G_{k+2},  c = 2 (k >= 1) or 1 (k = 0),
+// D_k = plane k of dBasis in the k-major layout [K][N][M][Fin] (written so by
+// the dy W^T GEMM); k = 0 writes dx [N][M][Fin] directly.
+struct ClenArgs {
+  const int* rowptr;
+  const int* col;
+  const float* val;
+  const int* rperm;
+  const float* Gn1;  // G_{k+1}
+  const float* Gn2;  // G_{k+2}
+  float* Gout;       // G_k (or dx when k == 0)
+  const float* Dk;   // D_k plane
+  int M, Fin, K, k;
+};
+
+template <int VEC>
+__global__ __launch_bounds__(256) void k_clenshaw_step(ClenArgs a, StepGeom g) {
+#pragma clang fp contract(off)
+  typedef Vec<VEC> V;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int n, rb;
+  block_coords(g, &n, &rb);
+  const int rsub = lane / g.lpr, lc = lane - rsub * g.lpr;
+  if (rsub >= g.rpw) return;
+  const int ri = (rb * 4 + wave) * g.rpw + rsub;
+  if (ri >= a.M) return;
+  const int r = a.rperm ? a.rperm[ri] : ri;
+  const int j0 = a.rowptr[r], j1 = a.rowptr[r + 1];
+  const int64_t sbase = int64_t(n) * a.M * a.Fin;
+  const int64_t rbase = sbase + int64_t(r) * a.Fin;
+  const bool has1 = (a.k + 1) <= (a.K - 1), has2 = (a.k + 2) <= (a.K - 1);
+  const float c = (a.k >= 1) ? 2.f : 1.f;
+  for (int f0 = lc * VEC; f0 < a.Fin; f0 += g.lpr * VEC) {
+    typename V::T acc = V::zero();
+    if (has1) acc = row_spmm<VEC>(a.col, a.val, j0, j1, a.Gn1 + sbase, a.Fin, f0);
+    typename V::T o = V::add_c_sub(V::ld(a.Dk + rbase + f0), c, acc);
+    if (has2) o = V::sub(o, V::ld(a.Gn2 + rbase + f0));
+    V::st(a.Gout + rbase + f0, o);
+  }
+}
+
+StepGeom step_geom(int N, int M, int Fin, int vec) {
+  StepGeom g;
+  const int lanes = (Fin + vec - 1) / vec;
+  g.lpr = lanes < 64 ? lanes : 64;
+  g.rpw = 64 / g.lpr;
+  g.rb = (M + 4 * g.rpw - 1) / (4 * g.rpw);
+  // sample-per-XCD mapping keeps each XCD's gathers inside one sample slab in
+  // its own 4 MB L2; slabs larger than that are better shared by all XCDs at
+  // once (all blocks of sample n before sample n+1) so the one slab being
+  // gathered stays in the 256 MB Infinity Cache
+  const int64_t slab = int64_t(M) * Fin * 4;
+  g.xcd_map = (N % 8 == 0 && slab <= (int64_t(2) << 20)) ? 1 : 0;
+  return g;
 }
 
 // C = op(A) op(B), 64x64 output tile per 256-thread block, each wave a 32x32
@@ -135,7 +387,8 @@ __global__ __launch_bounds__(256) void k_clenshaw(
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void k_gemm_f32(int Mg, int Ng, int Kg, const float* __restrict__ A,
                                                   int lda, const float* __restrict__ B, int ldb,
-                                                  float* __restrict__ C, int ldc, int kchunk) {
+                                                  float* __restrict__ C, int ldc, int kchunk,
+                                                  int remapK) {
   __shared__ float As[16][68];
   __shared__ float Bs[16][68];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -180,10 +433,15 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int Mg, int Ng, int Kg, const 
     __syncthreads();
   }
   const int col = n0 + wc * 32 + li;
+  // remapK > 0: column col = fin*K + k of row `row` goes to plane k of a
+  // [K][Mg][Ng/K] tensor (dBasis in the streaming backward's k-major layout)
+  const int rk = remapK > 0 ? remapK : 1;
+  const int64_t cidx = remapK > 0 ? int64_t(col % rk) * Mg * (Ng / rk) + col / rk : col;
+  const int64_t rstride = remapK > 0 ? int64_t(Ng / rk) : int64_t(ldc);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = m0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    if (row < Mg && col < Ng) C[size_t(row) * ldc + col] = acc[r];
+    if (row < Mg && col < Ng) C[int64_t(row) * rstride + cidx] = acc[r];
   }
 }
 
@@ -273,36 +531,67 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
 
 }  // namespace
 
-hipError_t launch_x_to_cols(const float* x, float* T0, float* basis, int N, int M, int Fin, int K,
-                            hipStream_t s) {
-  const int64_t total = int64_t(M) * N * Fin;
-  hipLaunchKernelGGL(k_x_to_cols, dim3(grid_for(total, 256)), dim3(256), 0, s, x, T0, basis, N, M,
-                     Fin, K);
+hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val, const int* rperm,
+                            const float* Tp, const float* Tpp, float* Tout, const float* x,
+                            const float* slots, float* basis, int N, int M, int Fin, int K, int k,
+                            bool last, hipStream_t s) {
+  ChebStepArgs a{rowptr, col, val, rperm, Tp, Tpp, Tout, x, slots,
+                 int64_t(N) * M * Fin, basis, M, Fin, K, k};
+  const int vec = (Fin % 4 == 0) ? 4 : 1;
+  const StepGeom g = step_geom(N, M, Fin, vec);
+  const dim3 grid(unsigned(int64_t(N) * g.rb)), block(256);
+  const size_t stage = size_t(4) * g.rpw * size_t(Fin) * K * sizeof(float);
+  if (last && stage <= size_t(64) * 1024) {
+    if (vec == 4) hipLaunchKernelGGL((k_cheb_last<4>), grid, block, stage, s, a, g);
+    else hipLaunchKernelGGL((k_cheb_last<1>), grid, block, stage, s, a, g);
+  } else if (vec == 4) {
+    if (last) hipLaunchKernelGGL((k_cheb_step<4, true>), grid, block, 0, s, a, g);
+    else hipLaunchKernelGGL((k_cheb_step<4, false>), grid, block, 0, s, a, g);
+  } else {
+    if (last) hipLaunchKernelGGL((k_cheb_step<1, true>), grid, block, 0, s, a, g);
+    else hipLaunchKernelGGL((k_cheb_step<1, false>), grid, block, 0, s, a, g);
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_spmm_cheb_step(const int* rowptr, const int* col, const float* val,
-                                 const float* Tprev, const float* Tprev2, float* Tout, float* basis,
-                                 int N, int M, int Fin, int K, int k, hipStream_t s) {
-  const int64_t B = int64_t(N) * Fin;
-  const dim3 grid((M + 3) / 4);
-  const bool vec4 = (B % 4 == 0) && (reinterpret_cast<uintptr_t>(Tprev) % 16 == 0) &&
-                    (!Tout || reinterpret_cast<uintptr_t>(Tout) % 16 == 0) &&
-                    (!Tprev2 || reinterpret_cast<uintptr_t>(Tprev2) % 16 == 0);
-  if (vec4)
-    hipLaunchKernelGGL(k_spmm_cheb<true>, grid, dim3(256), 0, s, rowptr, col, val, Tprev, Tprev2,
-                       Tout, basis, N, M, Fin, K, k);
-  else
-    hipLaunchKernelGGL(k_spmm_cheb<false>, grid, dim3(256), 0, s, rowptr, col, val, Tprev, Tprev2,
-                       Tout, basis, N, M, Fin, K, k);
+hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tval, const int* rperm,
+                           const float* Gn1, const float* Gn2, float* Gout, const float* Dk, int N,
+                           int M, int Fin, int K, int k, hipStream_t s) {
+  ClenArgs a{trowptr, tcol, tval, rperm, Gn1, Gn2, Gout, Dk, M, Fin, K, k};
+  const int vec = (Fin % 4 == 0) ? 4 : 1;
+  const StepGeom g = step_geom(N, M, Fin, vec);
+  const dim3 grid(unsigned(int64_t(N) * g.rb)), block(256);
+  if (vec == 4) hipLaunchKernelGGL((k_clenshaw_step<4>), grid, block, 0, s, a, g);
+  else hipLaunchKernelGGL((k_clenshaw_step<1>), grid, block, 0, s, a, g);
   return hipGetLastError();
 }
 
-hipError_t launch_clenshaw_step(const int* trowptr, const int* tcol, const float* tval,
-                                const float* Gn1, const float* Gn2, float* Gout, const float* dA,
-                                float* dx, int N, int M, int Fin, int K, int k, hipStream_t s) {
-  hipLaunchKernelGGL(k_clenshaw, dim3((M + 3) / 4), dim3(256), 0, s, trowptr, tcol, tval, Gn1, Gn2,
-                     Gout, dA, dx, N, M, Fin, K, k);
+bool rowgemm_ok(int Kc, int lda, int Nc) {
+  const int KC2 = ((Kc + 1) / 2 + 15) / 16 * 16;
+  const int NT = (Nc + 31) / 32;
+  return Kc >= 2 && Kc <= 256 && Nc >= 1 && NT <= 8 && lda % 4 == 0 &&
+         size_t(2) * KC2 * NT * 32 * 4 <= size_t(64) * 1024;
+}
+
+hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
+                          int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
+                          int64_t c_plane, hipStream_t s) {
+  RowGemmArgs a{A, R, Kc, lda, ((Kc + 1) / 2 + 15) / 16 * 16, B, bs_k, bs_j, bs_p, Nc, C, ldc, c_plane};
+  const int NT = (Nc + 31) / 32;
+  const size_t lds = size_t(2) * a.KC2 * NT * 32 * 4;
+  const int64_t ntiles = (R + 127) / 128;
+  const unsigned gx = unsigned(ntiles < 1024 ? ntiles : 1024);
+  const dim3 grid(gx, unsigned(planes)), block(256);
+  switch (NT) {
+    case 1: hipLaunchKernelGGL(k_rowgemm<1>, grid, block, lds, s, a); break;
+    case 2: hipLaunchKernelGGL(k_rowgemm<2>, grid, block, lds, s, a); break;
+    case 3: hipLaunchKernelGGL(k_rowgemm<3>, grid, block, lds, s, a); break;
+    case 4: hipLaunchKernelGGL(k_rowgemm<4>, grid, block, lds, s, a); break;
+    case 5: hipLaunchKernelGGL(k_rowgemm<5>, grid, block, lds, s, a); break;
+    case 6: hipLaunchKernelGGL(k_rowgemm<6>, grid, block, lds, s, a); break;
+    case 7: hipLaunchKernelGGL(k_rowgemm<7>, grid, block, lds, s, a); break;
+    default: hipLaunchKernelGGL(k_rowgemm<8>, grid, block, lds, s, a); break;
+  }
   return hipGetLastError();
 }
 
@@ -319,22 +608,22 @@ int gemm_effective_splits(int Kg, int splits) {
 
 hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, const float* A,
                            int lda, const float* B, int ldb, float* C, int ldc, int splits,
-                           hipStream_t s) {
+                           hipStream_t s, int remapK) {
   const int kchunk = gemm_kchunk(Kg, splits);
   const int nsplit = gemm_effective_splits(Kg, splits);
   const dim3 grid((Mg + 63) / 64, (Ng + 63) / 64, nsplit > 0 ? nsplit : 1);
   if (!trans_a && !trans_b)
     hipLaunchKernelGGL((k_gemm_f32<false, false>), grid, dim3(256), 0, s, Mg, Ng, Kg, A, lda, B,
-                       ldb, C, ldc, kchunk);
+                       ldb, C, ldc, kchunk, remapK);
   else if (!trans_a && trans_b)
     hipLaunchKernelGGL((k_gemm_f32<false, true>), grid, dim3(256), 0, s, Mg, Ng, Kg, A, lda, B,
-                       ldb, C, ldc, kchunk);
+                       ldb, C, ldc, kchunk, remapK);
   else if (trans_a && !trans_b)
     hipLaunchKernelGGL((k_gemm_f32<true, false>), grid, dim3(256), 0, s, Mg, Ng, Kg, A, lda, B,
-                       ldb, C, ldc, kchunk);
+                       ldb, C, ldc, kchunk, remapK);
   else
     hipLaunchKernelGGL((k_gemm_f32<true, true>), grid, dim3(256), 0, s, Mg, Ng, Kg, A, lda, B, ldb,
-                       C, ldc, kchunk);
+                       C, ldc, kchunk, remapK);
   return hipGetLastError();
 }
 

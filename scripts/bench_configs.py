@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Timing of the non-headline configurations of SURVEY.md §8d on one GPU
+(bench.py measures the headline config B).  One JSON line per config:
+
+  C1  20NEWS-like 10k-vertex graph, layer 1: N=128, Fin=1, K=5, Fout=32
+  C2  same graph, layer 2:                  N=128, Fin=32, K=5, Fout=32
+  D   Chung-Lu 2^18 vertices, nnz 4.19M:    N=--d-batch (default 32), Fin=Fout=64, K=3
+  E   gconv-LSTM layer on grid(32) 8-NN:    T=12, N=128, Fin=2, H=32, K=3 (fwd+bwd, BPTT)
+
+fwd / bwd are HIP-event timings (torch's current stream, where every C-ABI
+call is enqueued) of one chebyshev5 forward and backward (dx + dW), median of
+rounds; alg_GBps uses SURVEY.md §8d's algorithmic bytes.
+Usage: python scripts/bench_configs.py [C1 C2 D E] [--d-batch N]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import scipy.sparse
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+from cnn_graph_amd import ops  # noqa: E402
+from cnn_graph_amd.plan import ChebPlan  # noqa: E402
+
+
+def ev_ms(fn, reps=5, rounds=3):
+    vals = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        vals.append(e0.elapsed_time(e1) / reps)
+    return float(np.median(vals))
+
+
+def alg_bytes(M, nnz, B, K):
+    csr = 8 * nnz + 4 * (M + 1)
+    return (K - 1) * csr + 4 * M * B * (2 + 3 * (K - 2)), (K - 1) * csr + 4 * M * B * (3 + 5 * (K - 2))
+
+
+def filter_config(name, Lt, N, Fin, K, Fout, dev):
+    M = Lt.shape[0]
+    plan = ChebPlan(Lt, device=0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    x = torch.rand((N, M, Fin), device=dev, generator=g)
+    W = torch.randn((Fin * K, Fout), device=dev, generator=g) * 0.1
+    dy = torch.randn((N, M, Fout), device=dev, generator=g)
+    r = ops.ChebRunner(plan, N, Fin, K, Fout, dev)
+    r.forward(x, W)
+    r.backward(dy, W)
+    torch.cuda.synchronize()
+    reps = 5 if M * N * Fin > 1e8 else 20
+    f = ev_ms(lambda: r.forward(x, W), reps)
+    b = ev_ms(lambda: r.backward(dy, W), reps)
+    bf, bb = alg_bytes(M, plan.nnz, N * Fin, K)
+    return {"config": name, "M": M, "nnz": plan.nnz, "N": N, "Fin": Fin, "K": K, "Fout": Fout,
+            "path": r.path, "fwd_ms": round(f, 4), "bwd_ms": round(b, 4),
+            "samples_per_s": round(N / ((f + b) * 1e-3), 1),
+            "fwd_alg_GBps": round(bf / (f * 1e-3) / 1e9, 1),
+            "bwd_alg_GBps": round(bb / (b * 1e-3) / 1e9, 1)}
+
+
+def lstm_config(dev, T=12, N=128, Fin=2, H=32, K=3):
+    from cnn_graph_amd.gconv_lstm import GConvLSTMCell, layer
+    with np.load(os.path.join(ROOT, "tests", "golden", "golden_E.npz"), allow_pickle=False) as z:
+        M = int(z["M"])
+        Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
+    # L = L~ + I  (rescale_L(L, 2) = L - I gives back this L~)
+    L = (Lt + scipy.sparse.identity(M, dtype=np.float32, format="csr")).tocsr()
+    cell = GConvLSTMCell(H, laplacian=L, lmax=2, K=K, feat_in=Fin, device=dev)
+    M = L.shape[0]
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    xs = torch.rand((T, N, M, Fin), device=dev, generator=g)
+    gh = torch.randn((T, N, M, H), device=dev, generator=g)
+
+    def fwd():
+        with torch.no_grad():
+            layer(cell, xs)
+
+    def fwdbwd():
+        hs, _ = layer(cell, xs)
+        hs.backward(gh)
+
+    fwdbwd()
+    torch.cuda.synchronize()
+    f = ev_ms(fwd, 3)
+    fb = ev_ms(fwdbwd, 3)
+    return {"config": "E", "M": M, "T": T, "N": N, "Fin": Fin, "H": H, "K": K,
+            "fwd_ms": round(f, 3), "fwd_bwd_ms": round(fb, 3),
+            "samples_per_s": round(N / (fb * 1e-3), 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["C1", "C2", "D", "E"])
+    ap.add_argument("--d-batch", type=int, default=32)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from cnn_graph_amd.graph import rescale_L
+    for name in args.configs:
+        if name in ("C1", "C2"):
+            with np.load(os.path.join(ROOT, "tests", "golden", "golden_C.npz"), allow_pickle=False) as z:
+                M = int(z["M"])
+                Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
+            Fin = 1 if name == "C1" else 32
+            out = filter_config(name, Lt, 128, Fin, 5, 32, dev)
+        elif name == "D":
+            import synth_graphs
+            Lt = rescale_L(synth_graphs.config_d_laplacian(), 2)
+            out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev)
+        elif name == "E":
+            out = lstm_config(dev)
+        else:
+            raise SystemExit(f"unknown config {name}")
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
