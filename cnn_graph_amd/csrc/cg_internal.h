@@ -61,6 +61,8 @@ struct SlotLayout {
 };
 struct ResidentFwdArgs {
   int M, Fin, K, Fout, Mp, dbg;
+  const float* res;  // y epilogue: y = act(basis W + res) (res may be NULL)
+  int act;           // 0 = none, 1 = ReLU
   SlotLayout E;                        // L~
   const int* col;                      // CSR columns / values of L~ (tails)
   const float* val;
@@ -71,6 +73,7 @@ struct ResidentFwdArgs {
 };
 struct ResidentBwdArgs {
   int M, Fin, K, Fout, Mp, dbg;
+  int dx_acc;  // dx += result instead of dx = result
   SlotLayout E;                        // L~^T
   const int* col;                      // CSR of L~^T (tails)
   const float* val;
@@ -124,6 +127,8 @@ struct FastGeom {
 FastGeom fast_geometry(int M, int P, int max_row_nnz, int max_row_nnzT, int Fin, int K, int Fout);
 struct FastFwdArgs {
   int M, Fin, K, Fout, dbg;
+  const float* res;  // y epilogue: y = act(basis W + res) (res may be NULL)
+  int act;           // 0 = none, 1 = ReLU
   FastImage E;  // L~
   const float* x;
   const float* W;
@@ -132,6 +137,7 @@ struct FastFwdArgs {
 };
 struct FastBwdArgs {
   int M, Fin, K, Fout, Mp, dbg;
+  int dx_acc;  // dx += result instead of dx = result
   size_t dscratch_bytes;
   FastImage E;  // L~^T
   const float* dy;
@@ -155,7 +161,7 @@ hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val,
 // Reverse step G_k = D_k + c L~^T G_{k+1} - G_{k+2} (sample-major; k = 0 -> dx).
 hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tval, const int* rperm,
                            const float* Gn1, const float* Gn2, float* Gout, const float* Dk, int N,
-                           int M, int Fin, int K, int k, hipStream_t s);
+                           int M, int Fin, int K, int k, int dx_acc, hipStream_t s);
 // C[Mg x Ng] (+)= op(A)[Mg x Kg] * op(B)[Kg x Ng]; fp32 in/out on MFMA f32.
 // trans_a: A stored [Kg][lda] (A^T row-major); trans_b: B stored [Ng][ldb].
 // splits > 1: the K range is cut into `splits` slices, slice s writes
@@ -164,9 +170,10 @@ hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tva
 // C[p*c_plane + r*ldc + j] = sum_k A[r*lda + k] * B[p*bs_p + k*bs_k + j*bs_j],
 // r < R, k < Kc, j < Nc.  rowgemm_ok says whether the shape is supported.
 bool rowgemm_ok(int Kc, int lda, int Nc);
+// Epilogue (planes == 1 use): C = act(C + res), res [R][ldc] or NULL, act 1 = ReLU.
 hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
                           int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
-                          int64_t c_plane, hipStream_t s);
+                          int64_t c_plane, hipStream_t s, const float* res = nullptr, int act = 0);
 // remapK > 0: write C in the k-major [remapK][Mg][Ng/remapK] layout instead
 // (column fin*K + k -> plane k), splits must be 1.
 hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, const float* A,
@@ -184,6 +191,16 @@ hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, floa
 // Same fixed-order reduction, then out[i] = out[i] + sum (accumulate != 0).
 hipError_t launch_reduce_slabs_acc(const float* slab, int nslab, int64_t count, float* out,
                                    int accumulate, hipStream_t s);
+
+// ---- elementwise epilogues and the MSE loss (epilogue.hip) ---------------------
+// y = act(y + res) in place (res may be NULL); act 1 = ReLU
+hipError_t launch_act_fwd(float* y, const float* res, int act, int64_t n, hipStream_t s);
+// dz = y > 0 ? dy : 0 (gradient through ReLU given its output y)
+hipError_t launch_relu_bwd(const float* dy, const float* y, float* dz, int64_t n, hipStream_t s);
+// loss = mean((labels - pred)^2) (fixed-order reduction); dpred = 2 (pred - labels) / n
+int mse_chunks(int64_t n);
+hipError_t launch_mse(const float* pred, const float* labels, int64_t n, float* slab, float* loss,
+                      float* dpred, hipStream_t s);
 
 // ---- gconv-LSTM cell (lstm.hip) ------------------------------------------------
 // gates: 0 = reference gate functions (tan / sigmoid / sigmoid / tanh,

@@ -534,12 +534,18 @@ int cg_cheb_workspace_bytes(const cg_plan* plan, int32_t N, int32_t Fin, int32_t
   return ok();
 }
 
-int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
-                    const float* x, const float* W, float* basis, float* y, void* workspace,
-                    size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+// forward with the residual / activation epilogue y = act(basis W + res)
+int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout, const float* x,
+                 const float* W, const float* res, int act, float* basis, float* y, void* workspace,
+                 size_t ws_bytes, void* stream) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
   if (!x) return fail(CG_ERR_ARG, "null x");
+  if (act != CG_ACT_NONE && act != CG_ACT_RELU) return fail(CG_ERR_ARG, "unknown activation %d", act);
+  if (!y && (res || act)) return fail(CG_ERR_ARG, "an epilogue needs y");
   if (y && !W) return fail(CG_ERR_ARG, "null W with non-null y");
   if (!y && !basis) return fail(CG_ERR_ARG, "nothing to compute (basis and y both null)");
   if ((rc = check_device(plan))) return rc;
@@ -560,6 +566,8 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
     a.W = y ? W : nullptr;
     a.basis = basis;
     a.y = y;
+    a.res = res;
+    a.act = act;
     CG_HIP(cg::launch_fast_forward(fast_geom(plan, Fin, K, Fout), N, a, s));
     return ok();
   }
@@ -579,6 +587,8 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
     a.W = y ? W : nullptr;
     a.basis = basis;
     a.y = y;
+    a.res = res;
+    a.act = act;
     CG_HIP(cg::launch_resident_forward(g, N, a, s));
     return ok();
   }
@@ -604,19 +614,21 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
   }
   if (y) {
     const int FinK = Fin * K;
-    if (cg::rowgemm_ok(FinK, FinK, Fout))
+    if (cg::rowgemm_ok(FinK, FinK, Fout)) {
       CG_HIP(cg::launch_rowgemm(basis, int64_t(N) * M, FinK, FinK, W, Fout, 1, 0, 1, Fout, y, Fout,
-                                0, s));
-    else
+                                0, s, res, act));
+    } else {
       CG_HIP(cg::launch_gemm_f32(false, false, N * M, Fout, FinK, basis, FinK, W, Fout, y, Fout, 1,
                                  s));
+      if (res || act) CG_HIP(cg::launch_act_fwd(y, res, act, int64_t(N) * M * Fout, s));
+    }
   }
   return ok();
 }
 
-int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
-                     const float* dy, const float* basis, const float* W, float* dx, float* dW,
-                     void* workspace, size_t ws_bytes, void* stream) {
+int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout, const float* dy,
+                  const float* basis, const float* W, float* dx, int dx_acc, float* dW,
+                  void* workspace, size_t ws_bytes, void* stream) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
   if (!dy || !basis || !W) return fail(CG_ERR_ARG, "null dy/basis/W");
@@ -668,6 +680,7 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
       a.basis = basis;
       a.W = W;
       a.dx = dx;
+      a.dx_acc = dx_acc;
       a.dw_slab = fused ? slabs : nullptr;
       CG_HIP(cg::launch_fast_backward(g, N, a, s));
     } else if (path == CG_PATH_RESIDENT) {
@@ -686,6 +699,7 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
       a.dy = dy;
       a.W = W;
       a.dx = dx;
+      a.dx_acc = dx_acc;
       CG_HIP(cg::launch_resident_backward(g, N, a, s));
     } else {
       const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
@@ -706,7 +720,7 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
         CG_HIP(cg::launch_clenshaw(plan->trowptr, plan->tcol, plan->tval, rperm,
                                    (k + 1 <= K - 1) ? G(k + 1) : nullptr,
                                    (k + 2 <= K - 1) ? G(k + 2) : nullptr, k == 0 ? dx : G(k),
-                                   dA + size_t(k) * slot, N, M, Fin, K, k, s));
+                                   dA + size_t(k) * slot, N, M, Fin, K, k, dx_acc, s));
     }
   }
   if (!dW) return ok();
@@ -718,6 +732,68 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
   }
   if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
     CG_HIP(cg::launch_reduce_slabs(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, s));
+  return ok();
+}
+
+}  // namespace
+
+extern "C" {
+
+int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                    const float* x, const float* W, float* basis, float* y, void* workspace,
+                    size_t ws_bytes, void* stream) {
+  return forward_impl(plan, N, Fin, K, Fout, x, W, nullptr, CG_ACT_NONE, basis, y, workspace,
+                      ws_bytes, stream);
+}
+
+int cg_cheb_forward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                       const float* x, const float* W, const float* residual, int32_t act,
+                       float* basis, float* y, void* workspace, size_t ws_bytes, void* stream) {
+  return forward_impl(plan, N, Fin, K, Fout, x, W, residual, act, basis, y, workspace, ws_bytes,
+                      stream);
+}
+
+int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                     const float* dy, const float* basis, const float* W, float* dx, float* dW,
+                     void* workspace, size_t ws_bytes, void* stream) {
+  return backward_impl(plan, N, Fin, K, Fout, dy, basis, W, dx, 0, dW, workspace, ws_bytes, stream);
+}
+
+int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                        const float* dy, const float* y, int32_t act, const float* basis,
+                        const float* W, float* dx, int32_t dx_accumulate, float* dW, float* dz,
+                        void* workspace, size_t ws_bytes, void* stream) {
+  if (act != CG_ACT_NONE && act != CG_ACT_RELU) return fail(CG_ERR_ARG, "unknown activation %d", act);
+  if (!plan || !dy) return fail(CG_ERR_ARG, "null plan / dy");
+  const float* dy_eff = dy;
+  if (act == CG_ACT_RELU) {
+    if (!y || !dz) return fail(CG_ERR_ARG, "ReLU backward needs y (its output) and dz");
+    CG_HIP(cg::launch_relu_bwd(dy, y, dz, int64_t(N) * plan->M * Fout,
+                               reinterpret_cast<hipStream_t>(stream)));
+    dy_eff = dz;
+  } else if (dz) {
+    CG_HIP(hipMemcpyAsync(dz, dy, size_t(N) * plan->M * Fout * sizeof(float),
+                          hipMemcpyDeviceToDevice, reinterpret_cast<hipStream_t>(stream)));
+  }
+  if (!dx && !dW) return ok();
+  return backward_impl(plan, N, Fin, K, Fout, dy_eff, basis, W, dx, dx_accumulate != 0, dW,
+                       workspace, ws_bytes, stream);
+}
+
+int cg_mse_loss_workspace_bytes(int64_t n, size_t* bytes) {
+  if (!bytes || n < 1) return fail(CG_ERR_ARG, "mse_loss: bad arguments");
+  *bytes = al256(size_t(cg::mse_chunks(n)) * 4);
+  return ok();
+}
+
+int cg_mse_loss(const float* pred, const float* labels, int64_t n, float* loss, float* dpred,
+                void* workspace, size_t ws_bytes, void* stream) {
+  if (!pred || !labels || !loss || n < 1) return fail(CG_ERR_ARG, "mse_loss: bad arguments");
+  const size_t need = al256(size_t(cg::mse_chunks(n)) * 4);
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "mse_loss workspace too small: %zu < %zu", ws_bytes, need);
+  CG_HIP(cg::launch_mse(pred, labels, n, static_cast<float*>(workspace), loss, dpred,
+                        reinterpret_cast<hipStream_t>(stream)));
   return ok();
 }
 

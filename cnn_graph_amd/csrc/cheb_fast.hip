@@ -315,7 +315,12 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int m = tile * 32 + (e & 3) + 8 * (e >> 2) + 4 * c.h;
-            if (m < M && f < Fout) yn[size_t(m) * Fout + f] = c.acc[t][q][e];
+            if (m < M && f < Fout) {
+              float v = c.acc[t][q][e];
+              if (A.res) v = v + A.res[size_t(n) * M * Fout + size_t(m) * Fout + f];
+              if (A.act) v = v > 0.f ? v : 0.f;
+              yn[size_t(m) * Fout + f] = v;
+            }
           }
         }
       }
@@ -405,7 +410,7 @@ struct Bwd {
       if (A.dx && r.row >= 0) {
         float* d = A.dx + (size_t(n) * M + r.row) * FV;
 #pragma unroll
-        for (int fin = 0; fin < FV; ++fin) d[fin] = comp(g, fin);
+        for (int fin = 0; fin < FV; ++fin) d[fin] = A.dx_acc ? d[fin] + comp(g, fin) : comp(g, fin);
       }
     } else {
       lds_stv<FV>(ring + r.rb + CUR * 4 * FV, g);

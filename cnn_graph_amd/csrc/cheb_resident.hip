@@ -246,7 +246,12 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int m = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (m < M && f < Fout) yn[size_t(m) * Fout + f] = acc[t][q][r];
+            if (m < M && f < Fout) {
+              float v = acc[t][q][r];
+              if (A.res) v = v + A.res[size_t(n) * M * Fout + size_t(m) * Fout + f];
+              if (A.act) v = v > 0.f ? v : 0.f;
+              yn[size_t(m) * Fout + f] = v;
+            }
           }
         }
       }
@@ -387,7 +392,10 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(ResidentBwdArgs A) {
           float g = Dk[r] + c * a;
           if (i >= 2) g = g - lds_f(rp + NX2 * 4);
           if (k == 0) {
-            if (A.dx) A.dx[(size_t(n) * M + r) * Fin + fin] = g;
+            if (A.dx) {
+              float* d = A.dx + (size_t(n) * M + r) * Fin + fin;
+              *d = A.dx_acc ? *d + g : g;
+            }
           } else {
             lds_st(rp + CUR * 4, g);
           }

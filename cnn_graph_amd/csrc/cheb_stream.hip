@@ -79,6 +79,7 @@ struct Vec<1> {
     return d + c * a;
   }
   static __device__ __forceinline__ T sub(T a, T b) { return a - b; }
+  static __device__ __forceinline__ T add(T a, T b) { return a + b; }
 };
 template <>
 struct Vec<4> {
@@ -104,6 +105,9 @@ struct Vec<4> {
   static __device__ __forceinline__ T sub(T a, T b) {
 #pragma clang fp contract(off)
     return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+  }
+  static __device__ __forceinline__ T add(T a, T b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
   }
 };
 
@@ -256,6 +260,8 @@ struct RowGemmArgs {
   float* C;
   int ldc;
   int64_t c_plane;
+  const float* res;  // epilogue: C = act(C + res)
+  int act;
 };
 
 template <int NT>
@@ -318,7 +324,12 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (rr < a.R) C[rr * a.ldc + col] = acc[t][q];
+        if (rr < a.R) {
+          float v = acc[t][q];
+          if (a.res) v = v + a.res[rr * a.ldc + col];
+          if (a.act) v = v > 0.f ? v : 0.f;
+          C[rr * a.ldc + col] = v;
+        }
       }
     }
   }
@@ -338,6 +349,7 @@ struct ClenArgs {
   float* Gout;       // G_k (or dx when k == 0)
   const float* Dk;   // D_k plane
   int M, Fin, K, k;
+  int dx_acc;        // k == 0: dx += G_0
 };
 
 template <int VEC>
@@ -362,6 +374,7 @@ __global__ __launch_bounds__(256) void k_clenshaw_step(ClenArgs a, StepGeom g) {
     if (has1) acc = row_spmm<VEC>(a.col, a.val, j0, j1, a.Gn1 + sbase, a.Fin, f0);
     typename V::T o = V::add_c_sub(V::ld(a.Dk + rbase + f0), c, acc);
     if (has2) o = V::sub(o, V::ld(a.Gn2 + rbase + f0));
+    if (a.dx_acc && a.k == 0) o = V::add(V::ld(a.Gout + rbase + f0), o);
     V::st(a.Gout + rbase + f0, o);
   }
 }
@@ -556,8 +569,8 @@ hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val,
 
 hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tval, const int* rperm,
                            const float* Gn1, const float* Gn2, float* Gout, const float* Dk, int N,
-                           int M, int Fin, int K, int k, hipStream_t s) {
-  ClenArgs a{trowptr, tcol, tval, rperm, Gn1, Gn2, Gout, Dk, M, Fin, K, k};
+                           int M, int Fin, int K, int k, int dx_acc, hipStream_t s) {
+  ClenArgs a{trowptr, tcol, tval, rperm, Gn1, Gn2, Gout, Dk, M, Fin, K, k, dx_acc};
   const int vec = (Fin % 4 == 0) ? 4 : 1;
   const StepGeom g = step_geom(N, M, Fin, vec);
   const dim3 grid(unsigned(int64_t(N) * g.rb)), block(256);
@@ -575,8 +588,9 @@ bool rowgemm_ok(int Kc, int lda, int Nc) {
 
 hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
                           int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
-                          int64_t c_plane, hipStream_t s) {
-  RowGemmArgs a{A, R, Kc, lda, ((Kc + 1) / 2 + 15) / 16 * 16, B, bs_k, bs_j, bs_p, Nc, C, ldc, c_plane};
+                          int64_t c_plane, hipStream_t s, const float* res, int act) {
+  RowGemmArgs a{A, R, Kc, lda, ((Kc + 1) / 2 + 15) / 16 * 16, B, bs_k, bs_j, bs_p, Nc, C, ldc, c_plane,
+                res, act};
   const int NT = (Nc + 31) / 32;
   const size_t lds = size_t(2) * a.KC2 * NT * 32 * 4;
   const int64_t ntiles = (R + 127) / 128;

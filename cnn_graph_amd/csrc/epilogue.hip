@@ -1,0 +1,108 @@
+// Elementwise pieces of the residual GraphConv block and its training step
+// (lib/graph_conv.py:234-330, lib/graph_model.py:246-298), for the paths whose
+// contraction kernel does not apply them itself:
+//   k_act_fwd   y = act(y + res)              (b1relu of x + x_identity, :256-262)
+//   k_relu_bwd  dz = y > 0 ? dy : 0           (ReLU gradient from its output)
+//   k_mse_*     loss = mean((labels - pred)^2), dpred = 2 (pred - labels) / n
+//               (tf.reduce_mean(tf.square(tf.subtract(labels, logits))),
+//               lib/graph_model.py:255), fixed-order two-stage reduction.
+// The fast resident forward and the streaming row GEMM apply the residual /
+// ReLU epilogue in their own y store; these kernels are the fallback.
+#include "cg_internal.h"
+
+namespace cg {
+namespace {
+
+inline int grid1d(int64_t n, int per_block) {
+  int64_t g = (n + per_block - 1) / per_block;
+  return int(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+__global__ __launch_bounds__(256) void k_act_fwd(float* __restrict__ y, const float* __restrict__ res,
+                                                 int act, int64_t n) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    float v = y[i];
+    if (res) v = v + res[i];
+    if (act) v = v > 0.f ? v : 0.f;
+    y[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_relu_bwd(const float* __restrict__ dy,
+                                                  const float* __restrict__ y,
+                                                  float* __restrict__ dz, int64_t n) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+    dz[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+
+// Block z sums (labels - pred)^2 over its contiguous chunk (lanes strided,
+// then a fixed-order tree in LDS) and writes dpred for the same elements.
+__global__ __launch_bounds__(256) void k_mse_part(const float* __restrict__ pred,
+                                                  const float* __restrict__ labels, int64_t n,
+                                                  int64_t chunk, float inv2n,
+                                                  float* __restrict__ slab,
+                                                  float* __restrict__ dpred) {
+#pragma clang fp contract(off)
+  __shared__ float part[256];
+  const int64_t c0 = int64_t(blockIdx.x) * chunk;
+  const int64_t c1 = (c0 + chunk < n) ? c0 + chunk : n;
+  float s = 0.f;
+  for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
+    const float d = labels[i] - pred[i];
+    s = s + d * d;
+    if (dpred) dpred[i] = (pred[i] - labels[i]) * inv2n;
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (int(threadIdx.x) < w) part[threadIdx.x] = part[threadIdx.x] + part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) slab[blockIdx.x] = part[0];
+}
+
+__global__ __launch_bounds__(256) void k_mse_final(const float* __restrict__ slab, int nslab,
+                                                   float inv_n, float* __restrict__ loss) {
+#pragma clang fp contract(off)
+  __shared__ float part[256];
+  float s = 0.f;
+  for (int z = threadIdx.x; z < nslab; z += 256) s = s + slab[z];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (int(threadIdx.x) < w) part[threadIdx.x] = part[threadIdx.x] + part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = part[0] * inv_n;
+}
+
+}  // namespace
+
+hipError_t launch_act_fwd(float* y, const float* res, int act, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_act_fwd, dim3(grid1d(n, 256)), dim3(256), 0, s, y, res, act, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_relu_bwd(const float* dy, const float* y, float* dz, int64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_relu_bwd, dim3(grid1d(n, 256)), dim3(256), 0, s, dy, y, dz, n);
+  return hipGetLastError();
+}
+
+int mse_chunks(int64_t n) {
+  int64_t c = (n + 4095) / 4096;  // ~4096 elements per block, at most 1024 blocks
+  if (c > 1024) c = 1024;
+  return int(c < 1 ? 1 : c);
+}
+
+hipError_t launch_mse(const float* pred, const float* labels, int64_t n, float* slab, float* loss,
+                      float* dpred, hipStream_t s) {
+  const int chunks = mse_chunks(n);
+  const int64_t chunk = (n + chunks - 1) / chunks;
+  hipLaunchKernelGGL(k_mse_part, dim3(chunks), dim3(256), 0, s, pred, labels, n, chunk,
+                     float(2.0 / double(n)), slab, dpred);
+  hipLaunchKernelGGL(k_mse_final, dim3(1), dim3(256), 0, s, slab, chunks, float(1.0 / double(n)),
+                     loss);
+  return hipGetLastError();
+}
+
+}  // namespace cg

@@ -87,6 +87,23 @@ class GraphConv:
         W = self._weight_variable([Fin * K, Fout], regularization=False)
         return ops.cheb_conv(x, W, plan, int(K))
 
+    def _filter_act(self, x, L, Fout, K, residual=None):
+        """b1relu(filter(x) [+ residual]) -- fused into the filter's y store when
+        the bound filter / activation are chebyshev5 / b1relu (the residual
+        block's `x = filter(x)`, `x = x + x_identity`, `x = brelu(x)`,
+        lib/graph_conv.py:256-262); otherwise the separate calls."""
+        fuse = (getattr(self.filter, "__func__", None) is GraphConv.chebyshev5 and
+                getattr(self.brelu, "__func__", None) is GraphConv.b1relu)
+        if not fuse:
+            y = self.filter(x, L, Fout, K)
+            if residual is not None:
+                y = y + residual
+            return self.brelu(y)
+        N, M, Fin = (int(s) for s in x.shape)
+        plan = plan_for(L, lmax=2, device=x.device.index or 0, path=self.path)
+        W = self._weight_variable([Fin * K, Fout], regularization=False)
+        return ops.cheb_conv(x, W, plan, int(K), residual=residual, act="relu")
+
     # -- activations / pooling -----------------------------------------------------
     def b1relu(self, x):
         """lib/graph_conv.py:178-187 (its bias is commented out -> plain ReLU)."""
@@ -103,17 +120,14 @@ class GraphConv:
         x_identity = x
         with self.variable_scope(name_scope):
             with self.variable_scope("sublayer0" if residual else "sublayer0nores"):
-                x = self.brelu(self.filter(x, L, nfilter, K))
+                x = self._filter_act(x, L, nfilter, K)
             with self.variable_scope("sublayer1" if residual else "sublayer1nores"):
-                x = self.filter(x, L, nfilter, K)
-                if residual:
-                    x = x + x_identity
-                x = self.brelu(x)
+                x = self._filter_act(x, L, nfilter, K, x_identity if residual else None)
         return x
 
     def residual_network(self, x, L, nfilter, K, nres_layer_count, Fout_last=2):
         with self.variable_scope("conv_init"):
-            x = self.brelu(self.filter(x, L, nfilter, K))
+            x = self._filter_act(x, L, nfilter, K)
         for i in range(nres_layer_count):
             x = self.residual_layer(x, L, nfilter, K, f"residual_layer_{i}")
         with self.variable_scope("convN"):

@@ -47,11 +47,15 @@ def _check_out(name, t, shape):
                          f"got {tuple(t.shape)}")
 
 
+ACTS = {"none": _lib.CG_ACT_NONE, "relu": _lib.CG_ACT_RELU}
+
+
 def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int,
                  want_basis: bool = True, out_basis: torch.Tensor | None = None,
-                 out_y: torch.Tensor | None = None):
-    """Basis (N*M, Fin*K) and y = basis @ W (N, M, Fout).  W None -> basis only.
-    out_basis / out_y: pre-allocated contiguous outputs of those shapes."""
+                 out_y: torch.Tensor | None = None, residual: torch.Tensor | None = None,
+                 act: str = "none"):
+    """Basis (N*M, Fin*K) and y = act(basis @ W + residual) (N, M, Fout).
+    W None -> basis only.  out_basis / out_y: pre-allocated contiguous outputs."""
     _check_dev("x", x)
     x = x.contiguous()
     N, M, Fin = x.shape
@@ -76,10 +80,15 @@ def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int
     if W is not None:
         y = out_y if out_y is not None else torch.empty((N, M, Fout), device=dev, dtype=torch.float32)
         _check_out("out_y", y, (N * M * Fout,))
+    if residual is not None:
+        _check_dev("residual", residual)
+        residual = residual.contiguous()
+        if W is None or residual.numel() != N * M * Fout:
+            raise ValueError(f"residual must be [N, M, Fout] = [{N}, {M}, {Fout}]")
     fwd_ws, _ = plan.workspace_bytes(N, Fin, K, Fout)
     ws = torch.empty(max(fwd_ws, 1), device=dev, dtype=torch.uint8)
-    _lib.call("cg_cheb_forward", plan.handle, N, Fin, K, Fout, _p(x), _p(W), _p(basis), _p(y),
-              _p(ws), fwd_ws, _stream(x))
+    _lib.call("cg_cheb_forward_ex", plan.handle, N, Fin, K, Fout, _p(x), _p(W), _p(residual),
+              ACTS[act], _p(basis), _p(y), _p(ws), fwd_ws, _stream(x))
     return basis, y
 
 
@@ -99,6 +108,52 @@ def cheb_backward(plan: ChebPlan, dy: torch.Tensor, basis: torch.Tensor, W: torc
     _lib.call("cg_cheb_backward", plan.handle, N, Fin, K, Fout, _p(dy), _p(basis), _p(W.contiguous()),
               _p(dx), _p(dW), _p(ws), bwd_ws, _stream(dy))
     return dx, dW
+
+
+def cheb_backward_ex(plan: ChebPlan, dy: torch.Tensor, y: torch.Tensor | None, act: str,
+                     basis: torch.Tensor, W: torch.Tensor, K: int, dx: torch.Tensor | None = None,
+                     dx_accumulate: bool = False, need_dx: bool = True, need_dW: bool = True):
+    """Backward through y = act(basis W + residual): returns (dx, dW, dz) where
+    dz = dy * act'(y) is also the gradient of the residual input.  With
+    dx_accumulate the input gradient is added into the given ``dx``."""
+    _check_dev("dy", dy)
+    dy = dy.contiguous()
+    N, M, Fout = dy.shape
+    FinK = int(W.shape[0])
+    Fin = FinK // K
+    dev = dy.device
+    if need_dx and dx is None:
+        if dx_accumulate:
+            raise ValueError("dx_accumulate needs a dx tensor")
+        dx = torch.empty((N, M, Fin), device=dev, dtype=torch.float32)
+    if dx is not None:
+        _check_out("dx", dx, (N, M, Fin))
+    dW = torch.empty((FinK, Fout), device=dev, dtype=torch.float32) if need_dW else None
+    dz = torch.empty((N, M, Fout), device=dev, dtype=torch.float32)
+    _, bwd_ws = plan.workspace_bytes(N, Fin, K, Fout)
+    ws = torch.empty(max(bwd_ws, 1), device=dev, dtype=torch.uint8)
+    _lib.call("cg_cheb_backward_ex", plan.handle, N, Fin, K, Fout, _p(dy), _p(y), ACTS[act],
+              _p(basis), _p(W.contiguous()), _p(dx if need_dx else None), int(dx_accumulate),
+              _p(dW), _p(dz), _p(ws), bwd_ws, _stream(dy))
+    return (dx if need_dx else None), dW, dz
+
+
+def mse_loss(pred: torch.Tensor, labels: torch.Tensor, need_grad: bool = True):
+    """lib/graph_model.py:255 mean((labels - pred)^2) on device: (loss [1], dpred or None)."""
+    _check_dev("pred", pred)
+    _check_dev("labels", labels)
+    pred, labels = pred.contiguous(), labels.contiguous()
+    if pred.numel() != labels.numel():
+        raise ValueError("pred and labels differ in size")
+    n = pred.numel()
+    nb = ctypes.c_size_t()
+    _lib.call("cg_mse_loss_workspace_bytes", n, ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 1), device=pred.device, dtype=torch.uint8)
+    loss = torch.empty((1,), device=pred.device, dtype=torch.float32)
+    dpred = torch.empty_like(pred) if need_grad else None
+    _lib.call("cg_mse_loss", _p(pred), _p(labels), n, _p(loss), _p(dpred), _p(ws), nb.value,
+              _stream(pred))
+    return loss, dpred
 
 
 class ChebRunner:
@@ -159,8 +214,29 @@ class ChebConv(torch.autograd.Function):
         return dx, dW, None, None
 
 
-def cheb_conv(x, W, plan: ChebPlan, K: int):
-    return ChebConv.apply(x, W, plan, K)
+class ChebConvAct(torch.autograd.Function):
+    """y = act(chebyshev5(x; L~, W, K) + residual) in one kernel pass
+    (lib/graph_conv.py:256-262); residual may be None."""
+
+    @staticmethod
+    def forward(ctx, x, W, residual, plan: ChebPlan, K: int, act: str):
+        basis, y = cheb_forward(plan, x, W, K, want_basis=True, residual=residual, act=act)
+        ctx.save_for_backward(basis, W, y)
+        ctx.plan, ctx.K, ctx.act, ctx.has_res = plan, K, act, residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        basis, W, y = ctx.saved_tensors
+        dx, dW, dz = cheb_backward_ex(ctx.plan, dy, y, ctx.act, basis, W, ctx.K,
+                                      need_dx=ctx.needs_input_grad[0])
+        return dx, dW, (dz if ctx.has_res else None), None, None, None
+
+
+def cheb_conv(x, W, plan: ChebPlan, K: int, residual=None, act: str = "none"):
+    if residual is None and act == "none":
+        return ChebConv.apply(x, W, plan, K)
+    return ChebConvAct.apply(x, W, residual, plan, K, act)
 
 
 class _MaxPool(torch.autograd.Function):

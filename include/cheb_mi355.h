@@ -108,6 +108,32 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
                      float* dx, float* dW, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Residual GraphConv block epilogues (lib/graph_conv.py:234-262):
+ *   y = act(basis W + residual)       residual [N][M][Fout] or NULL, act CG_ACT_*
+ * i.e. `x = self.filter(x, ...)`, `x = x + x_identity`, `x = b1relu(x)` in one
+ * pass (the resident and streaming kernels apply it in their y store).
+ * Backward through it: dz = dy * act'(y) with y the forward's OUTPUT (ReLU:
+ * y > 0), written to dz (required when act != NONE; also the gradient of the
+ * residual input), then the filter backward on dz.  dx_accumulate != 0 adds
+ * the filter's input gradient into dx (dx += ...) -- the gradient sum of a
+ * tensor that feeds both a filter and a residual branch.
+ * ------------------------------------------------------------------------- */
+enum { CG_ACT_NONE = 0, CG_ACT_RELU = 1 };
+int cg_cheb_forward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                       const float* x, const float* W, const float* residual, int32_t act,
+                       float* basis, float* y, void* workspace, size_t ws_bytes, void* stream);
+int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                        const float* dy, const float* y, int32_t act, const float* basis,
+                        const float* W, float* dx, int32_t dx_accumulate, float* dW, float* dz,
+                        void* workspace, size_t ws_bytes, void* stream);
+/* MSE loss of lib/graph_model.py:255, tf.reduce_mean(tf.square(labels - logits)),
+ * over n elements: *loss (device scalar) and dpred = 2 (pred - labels) / n
+ * (NULL to skip).  Fixed-order reduction (bitwise reproducible). */
+int cg_mse_loss_workspace_bytes(int64_t n, size_t* bytes);
+int cg_mse_loss(const float* pred, const float* labels, int64_t n, float* loss, float* dpred,
+                void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Weight gradient of the contraction on its own (the tf.matmul gradient of
  * lib/graph_conv.py:175 / lib/filter.py:93): dW = basis^T dy over R rows,
  * basis [R][FinK], dy [R][Fout], dW [FinK][Fout].  Fixed-order, bitwise

@@ -1,0 +1,139 @@
+"""Residual GraphConv block epilogues and the ResGNN training step on the GPU
+ vs the float64 oracles.  Bar: 1e-5 max-abs-normalised."""
+import numpy as np
+import pytest
+import scipy.sparse
+
+from conftest import case, load_golden
+from oracle import cheb_oracle as O
+from oracle import model_oracle as MO
+from oracle.lstm_oracle import cheb_conv64
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def dev(built_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_graph_amd import _lib
+    _lib.lib()
+    return torch.device("cuda", 0)
+
+
+def t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+
+
+def f64(x):
+    return x.detach().cpu().numpy().astype(np.float64)
+
+
+def golden_L(name):
+    c = case(load_golden(name))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    L = (Lt + scipy.sparse.identity(M, dtype=np.float32, format="csr")).tocsr()  # rescale_L(L,2) = Lt
+    return L, c
+
+
+@pytest.mark.parametrize("path,Fin,Fout", [("resident", 1, 16), ("resident", 4, 32),
+                                           ("resident", 3, 40), ("stream", 8, 32)])
+def test_forward_epilogue_and_backward_ex(dev, path, Fin, Fout):
+    """y = relu(basis W + res) (fast / classic / streaming kernels), then the
+    backward through it with dx accumulation."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    L, c = golden_L("golden_B.npz")
+    plan = ChebPlan.from_laplacian(L, 2, 0, path=path)
+    lap = (plan.rowptr, plan.col, plan.val.astype(np.float64))
+    rng = np.random.default_rng(Fin + Fout)
+    N, M, K = 4, plan.M, 6
+    x = rng.standard_normal((N, M, Fin))
+    W = rng.standard_normal((Fin * K, Fout)) * 0.2
+    res = rng.standard_normal((N, M, Fout))
+    dy = rng.standard_normal((N, M, Fout))
+    dx0 = rng.standard_normal((N, M, Fin))
+    basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), K, residual=t(res, dev), act="relu")
+    dxt = t(dx0, dev)
+    dx, dW, dz = ops.cheb_backward_ex(plan, t(dy, dev), y, "relu", basis, t(W, dev), K, dx=dxt,
+                                      dx_accumulate=True)
+    torch.cuda.synchronize()
+    xf = x.astype(np.float32).astype(np.float64)
+    A, yl = cheb_conv64(xf, lap, W.astype(np.float32).astype(np.float64), K)
+    pre = yl + res.astype(np.float32)
+    ref_y = np.maximum(pre, 0)
+    assert O.normwise_err(f64(y), ref_y) < TOL
+    ref_dz = dy.astype(np.float32) * (f64(y) > 0)
+    assert np.array_equal(f64(dz), ref_dz.astype(np.float32).astype(np.float64))
+    rdx, rdW = O.cheb_backward(ref_dz, A, W.astype(np.float32), lap[0], lap[1], lap[2], N, M, Fin, K)
+    assert O.normwise_err(f64(dx), rdx + dx0.astype(np.float32)) < TOL
+    assert O.normwise_err(f64(dW), rdW) < TOL
+
+
+def test_mse_loss_and_grad(dev):
+    from cnn_graph_amd import ops
+    rng = np.random.default_rng(3)
+    p = rng.standard_normal((64, 976, 2)).astype(np.float32)
+    lab = rng.standard_normal((64, 976, 2)).astype(np.float32)
+    loss, d = ops.mse_loss(t(p, dev), t(lab, dev))
+    torch.cuda.synchronize()
+    rl, rd = MO.loss_and_grad(p.astype(np.float64), lab)
+    assert abs(float(loss.item()) - rl) <= 1e-6 * rl
+    assert O.normwise_err(f64(d), rd) < TOL
+
+
+@pytest.mark.parametrize("graph,R,Fin,F", [("golden_B.npz", 1, 1, 16), ("golden_E.npz", 2, 2, 32)])
+def test_resgnn_train_steps_vs_oracle(dev, graph, R, Fin, F):
+    """Three ResGNN optimizer steps (forward, MSE, backward, Adam) vs the oracle:
+    loss, every gradient, every updated weight."""
+    from cnn_graph_amd.model import ResGNN
+    L, _ = golden_L(graph)
+    N, K = 4, 5
+    model = ResGNN(L, N=N, Fin=Fin, nfilter=F, K=K, nres_layer_count=R, learning_rate=1e-2,
+                   decay_rate=0.95, decay_steps=2, device=dev, seed=5)
+    lap = (model.plan.rowptr, model.plan.col, model.plan.val.astype(np.float64))
+    rng = np.random.default_rng(9)
+    x = rng.random((N, model.M, Fin)).astype(np.float32)
+    labels = rng.random((N, model.M, 2)).astype(np.float32)
+    Ws = [f64(w) for w in model.W]
+    state = [(np.zeros_like(w), np.zeros_like(w)) for w in Ws]
+    for step in range(1, 4):
+        loss = model.train_step(t(x, dev), t(labels, dev))
+        torch.cuda.synchronize()
+        lr = model.learning_rate(step - 1)
+        rl, rdW, Ws, state = MO.train_step(x.astype(np.float64), labels, Ws, lap, K, R, state, step, lr)
+        assert abs(float(loss.item()) - rl) <= 1e-5 * rl, (step, float(loss.item()), rl)
+        for name, g, rg in zip(model.names, model.dW, rdW):
+            assert O.normwise_err(f64(g), rg) < TOL, (step, name)
+        for name, w, rw in zip(model.names, model.W, Ws):
+            assert O.normwise_err(f64(w), rw) < TOL, (step, name)
+
+
+def test_graphconv_residual_network_autograd_matches_trainer(dev):
+    """GraphConv.residual_network (torch autograd over the fused epilogue ops)
+    gives the same gradients as the explicit ResGNN schedule."""
+    from cnn_graph_amd.graph_conv import GraphConv
+    from cnn_graph_amd.model import ResGNN
+    from cnn_graph_amd import ops
+    L, _ = golden_L("golden_B.npz")
+    N, K, F, R = 3, 4, 16, 1
+    model = ResGNN(L, N=N, Fin=1, nfilter=F, K=K, nres_layer_count=R, device=dev, seed=1)
+    gc = GraphConv(device=dev)
+    rng = np.random.default_rng(2)
+    x = t(rng.random((N, model.M, 1)), dev)
+    labels = t(rng.random((N, model.M, 2)), dev)
+    out = gc.residual_network(x, L, F, K, R, Fout_last=2)
+    for name, w in model.parameters().items():   # same weights in both
+        with torch.no_grad():
+            gc.weights[name].copy_(w)
+    out = gc.residual_network(x, L, F, K, R, Fout_last=2)
+    loss, _ = ops.mse_loss(out.detach(), labels, need_grad=False)
+    ((out - labels) ** 2).mean().backward()
+    model.train_step(x, labels)
+    torch.cuda.synchronize()
+    for name, g in model.gradients().items():
+        assert O.normwise_err(f64(gc.weights[name].grad), f64(g)) < 1e-5, name
