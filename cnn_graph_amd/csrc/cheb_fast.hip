@@ -121,12 +121,14 @@ struct Row {
   float v[kFastWidth];
 
   template <int FV>
-  __device__ __forceinline__ void load(const FastImage& E, int tid) {
+  __device__ __forceinline__ void load(const FastImage& E, int tid, int wl) {
     constexpr int REC = 12 * FV;
     row = E.row[tid];
     rb = E.rpos[tid] * REC;
     rb1 = E.rpos1[tid] * REC;
     rr = E.rposr[tid] * REC;
+    (void)wl;  // loading only the first wl slots was measured SLOWER (per-slot
+               // branches serialise the loads): load all 16 unconditionally
 #pragma unroll
     for (int j = 0; j < kFastWidth; ++j) {
       ca[j] = E.cpos[j * kT + tid] * REC;
@@ -253,13 +255,13 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
   F c(A, smem, tid);
   const int M = c.M, Fout = c.Fout, FinK = c.FinK;
 
-  c.r.template load<FV>(A.E, tid);
+  const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[c.wave]);
+  c.r.template load<FV>(A.E, tid, wl);
 #pragma unroll
   for (int t = 0; t < F::MT; ++t) {
     const int tile = imin(c.wave + t * kW, c.ntiles - 1);
     c.mb[t] = A.E.mpos[tile * 32 + c.li] * REC;
   }
-  const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[c.wave]);
   for (int i = tid; i < FinK * Fout; i += kT) c.s_W[i] = A.W ? A.W[i] : 0.f;
   // T_0 = x into ring slot 0 ([pos][0][fin]); zero record kept at 0
   const float* xn = A.x + size_t(n) * M * FV;
@@ -524,8 +526,8 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
   }
   // the row registers and the first dW operands are loaded after phase A,
   // whose dy tiles occupy 32 registers per lane until then
-  c.r.template load<FV>(A.E, tid);
   const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[wave]);
+  c.r.template load<FV>(A.E, tid, wl);
   if (DW) {
     // rows of this wave: 16 near-equal even-sized chunks of [0, M)
     const int q = ((M + 2 * kW - 1) / (2 * kW)) * 2;
