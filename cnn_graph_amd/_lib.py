@@ -16,7 +16,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cheb_mi355.h")
 
 CG_OK, CG_ERR_ARG, CG_ERR_HIP, CG_ERR_UNSUPPORTED, CG_ERR_ALLOC, CG_ERR_COMM = range(6)
 CG_PATH_AUTO, CG_PATH_RESIDENT, CG_PATH_STREAM = 0, 1, 2
-CG_ACT_NONE, CG_ACT_RELU = 0, 1
+CG_ACT_NONE, CG_ACT_RELU, CG_ACT_TANH = 0, 1, 2
 PATHS = {"auto": CG_PATH_AUTO, "resident": CG_PATH_RESIDENT, "stream": CG_PATH_STREAM}
 
 
@@ -57,6 +57,18 @@ _SIGNATURES = {
     "cg_weight_grad": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
     "cg_bias_grad_workspace_bytes": ([_c_i64, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
     "cg_bias_grad": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
+    "cg_bias_act_forward": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp], _c_int),
+    "cg_bias_act_workspace_bytes": ([_c_i64, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
+    "cg_bias_act_backward": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _c_i32, _vp, _c_sz, _vp],
+                             _c_int),
+    "cg_gemm_f32": ([_c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _c_i32, _vp, _c_i32, _vp, _c_i32,
+                     _vp], _c_int),
+    "cg_fourier_workspace_bytes": ([_c_i32, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_sz),
+                                    ctypes.POINTER(_c_sz)], _c_int),
+    "cg_fourier_forward": ([_c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _c_sz, _vp],
+                           _c_int),
+    "cg_fourier_backward": ([_c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_sz,
+                             _vp], _c_int),
     "cg_lstm_cell_forward": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
                              _c_int),
     "cg_lstm_cell_backward": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],

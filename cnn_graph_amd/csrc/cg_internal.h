@@ -197,6 +197,12 @@ hipError_t launch_reduce_slabs_acc(const float* slab, int nslab, int64_t count, 
 hipError_t launch_act_fwd(float* y, const float* res, int act, int64_t n, hipStream_t s);
 // dz = y > 0 ? dy : 0 (gradient through ReLU given its output y)
 hipError_t launch_relu_bwd(const float* dy, const float* y, float* dz, int64_t n, hipStream_t s);
+// y = act(x + bias[i % blen]) (bias may be NULL); act 0 none, 1 ReLU, 2 tanh
+hipError_t launch_bias_act_fwd(const float* x, const float* bias, int64_t blen, int act, int64_t n,
+                               float* y, hipStream_t s);
+// dz = dy * act'(y) given the activation's output y
+hipError_t launch_bias_act_bwd(const float* dy, const float* y, int act, int64_t n, float* dz,
+                               hipStream_t s);
 // loss = mean((labels - pred)^2) (fixed-order reduction); dpred = 2 (pred - labels) / n
 int mse_chunks(int64_t n);
 hipError_t launch_mse(const float* pred, const float* labels, int64_t n, float* slab, float* loss,
@@ -215,6 +221,20 @@ hipError_t launch_lstm_bwd(int gates, int64_t R, int H, const float* dh, const f
 // Column sums of A [R][C] as [colsum_chunks(R)][C] partial slabs.
 int colsum_chunks(int64_t R);
 hipError_t launch_colsum_slabs(const float* A, int64_t R, int C, float* slab, hipStream_t s);
+
+// ---- Fourier filter (fourier.hip) -----------------------------------------------
+// out[b][c][r] = in[b][r][c] for b < B, r < R, c < C (LDS-tiled)
+hipError_t launch_transpose_batched(const float* in, int64_t B, int R, int C, float* out,
+                                    hipStream_t s);
+// Yh[n][fo][m] = sum_fin W[m][fo][fin] Xh[n][fin][m]   (per-vertex filter)
+hipError_t launch_fourier_mix(const float* Xh, const float* W, int N, int M, int Fin, int Fout,
+                              float* Yh, hipStream_t s);
+// dXh[n][fin][m] = sum_fo W[m][fo][fin] dYh[n][fo][m]
+hipError_t launch_fourier_mix_t(const float* dYh, const float* W, int N, int M, int Fin, int Fout,
+                                float* dXh, hipStream_t s);
+// dW[m][fo][fin] = sum_n dYh[n][fo][m] Xh[n][fin][m]   (fixed order over n)
+hipError_t launch_fourier_dw(const float* dYh, const float* Xh, int N, int M, int Fin, int Fout,
+                             float* dW, hipStream_t s);
 
 // ---- misc ----------------------------------------------------------------------
 hipError_t launch_perm_gather(const float* x, const int32_t* perm, int N, int M_in, int M_out,

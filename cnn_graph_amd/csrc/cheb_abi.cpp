@@ -837,6 +837,146 @@ int cg_bias_grad(int64_t R, int32_t C, const float* dy, float* db, int32_t accum
   return ok();
 }
 
+// ---- bias + activation (b1relu / b1tanh / b2relu) and fc GEMM -----------------
+int cg_bias_act_forward(int64_t n, int32_t bias_len, const float* x, const float* bias,
+                        int32_t act, float* y, void* stream) {
+  if (!x || !y || n < 1) return fail(CG_ERR_ARG, "bias_act_forward: bad arguments");
+  if (act < CG_ACT_NONE || act > CG_ACT_TANH) return fail(CG_ERR_ARG, "unknown activation %d", act);
+  if (bias && (bias_len < 1 || n % bias_len))
+    return fail(CG_ERR_ARG, "bias_act_forward: n=%lld is not a multiple of bias_len=%d",
+                (long long)n, bias_len);
+  CG_HIP(cg::launch_bias_act_fwd(x, bias, bias ? bias_len : 1, act, n, y,
+                                 reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_bias_act_workspace_bytes(int64_t n, int32_t bias_len, size_t* bytes) {
+  if (!bytes || n < 1 || bias_len < 1 || n % bias_len)
+    return fail(CG_ERR_ARG, "bias_act_workspace_bytes: bad arguments");
+  *bytes = al256(size_t(cg::colsum_chunks(n / bias_len)) * size_t(bias_len) * 4);
+  return ok();
+}
+
+int cg_bias_act_backward(int64_t n, int32_t bias_len, const float* dy, const float* y, int32_t act,
+                         float* dz, float* db, int32_t accumulate, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  if (!dy || !dz || n < 1) return fail(CG_ERR_ARG, "bias_act_backward: bad arguments");
+  if (act < CG_ACT_NONE || act > CG_ACT_TANH) return fail(CG_ERR_ARG, "unknown activation %d", act);
+  if (act != CG_ACT_NONE && !y) return fail(CG_ERR_ARG, "bias_act_backward: activation needs y");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  CG_HIP(cg::launch_bias_act_bwd(dy, y, act, n, dz, s));
+  if (!db) return ok();
+  if (bias_len < 1 || n % bias_len)
+    return fail(CG_ERR_ARG, "bias_act_backward: n=%lld is not a multiple of bias_len=%d",
+                (long long)n, bias_len);
+  const int64_t R = n / bias_len;
+  const size_t need = al256(size_t(cg::colsum_chunks(R)) * size_t(bias_len) * 4);
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "bias_act workspace too small: %zu < %zu", ws_bytes, need);
+  float* slabs = static_cast<float*>(workspace);
+  CG_HIP(cg::launch_colsum_slabs(dz, R, bias_len, slabs, s));
+  CG_HIP(cg::launch_reduce_slabs_acc(slabs, cg::colsum_chunks(R), bias_len, db, accumulate != 0, s));
+  return ok();
+}
+
+int cg_gemm_f32(int32_t trans_a, int32_t trans_b, int32_t M, int32_t N, int32_t K, const float* A,
+                int32_t lda, const float* B, int32_t ldb, float* C, int32_t ldc, void* stream) {
+  if (!A || !B || !C || M < 1 || N < 1 || K < 1) return fail(CG_ERR_ARG, "gemm_f32: bad arguments");
+  if (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N) || ldc < N)
+    return fail(CG_ERR_ARG, "gemm_f32: leading dimension too small (lda=%d ldb=%d ldc=%d)", lda, ldb,
+                ldc);
+  if ((M + 63) / 64 > 2147483647 / 2 || (N + 63) / 64 > 65535)
+    return fail(CG_ERR_ARG, "gemm_f32: N=%d too large for the grid", N);
+  CG_HIP(cg::launch_gemm_f32(trans_a != 0, trans_b != 0, M, N, K, A, lda, B, ldb, C, ldc, 1,
+                             reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+// ---- Fourier filter (lib/graph_conv.py:83-111) ----------------------------------
+static bool fourier_shape_ok(int32_t N, int32_t M, int32_t Fin, int32_t Fout) {
+  if (N < 1 || M < 1 || Fin < 1 || Fout < 1 || N > 65535) return false;
+  const int64_t big = int64_t(N) * (Fin > Fout ? Fin : Fout) * M;
+  return big < (int64_t(1) << 31) && M <= 65535 * 32;
+}
+
+static void fourier_ws(int32_t N, int32_t M, int32_t Fin, int32_t Fout, size_t* fwd, size_t* bwd) {
+  const size_t xin = size_t(N) * Fin * M * 4, yout = size_t(N) * Fout * M * 4;
+  if (fwd) *fwd = (Fin > 1 ? al256(xin) : 0) + al256(yout) + (Fout > 1 ? al256(yout) : 0);
+  if (bwd) *bwd = (Fout > 1 ? al256(yout) : 0) + al256(yout) + al256(xin) + (Fin > 1 ? al256(xin) : 0);
+}
+
+int cg_fourier_workspace_bytes(int32_t N, int32_t M, int32_t Fin, int32_t Fout, size_t* fwd_bytes,
+                               size_t* bwd_bytes) {
+  if (!fourier_shape_ok(N, M, Fin, Fout)) return fail(CG_ERR_ARG, "fourier: bad shape");
+  fourier_ws(N, M, Fin, Fout, fwd_bytes, bwd_bytes);
+  return ok();
+}
+
+int cg_fourier_forward(int32_t N, int32_t M, int32_t Fin, int32_t Fout, const float* U,
+                       const float* W, const float* x, float* xhat, float* y, void* workspace,
+                       size_t ws_bytes, void* stream) {
+  if (!U || !W || !x || !xhat || !y) return fail(CG_ERR_ARG, "fourier_forward: null pointer");
+  if (!fourier_shape_ok(N, M, Fin, Fout)) return fail(CG_ERR_ARG, "fourier_forward: bad shape");
+  size_t need;
+  fourier_ws(N, M, Fin, Fout, &need, nullptr);
+  if (ws_bytes < need || (need && !workspace))
+    return fail(CG_ERR_ARG, "fourier_forward workspace too small: %zu < %zu", ws_bytes, need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* w = static_cast<char*>(workspace);
+  const size_t xin = size_t(N) * Fin * M * 4, yout = size_t(N) * Fout * M * 4;
+  const float* xs = x;
+  if (Fin > 1) {  // [N][M][Fin] -> [N][Fin][M]
+    float* xt = reinterpret_cast<float*>(w);
+    w += al256(xin);
+    CG_HIP(cg::launch_transpose_batched(x, N, M, Fin, xt, s));
+    xs = xt;
+  }
+  float* Yh = reinterpret_cast<float*>(w);
+  w += al256(yout);
+  // Xh = x U  (every signal row against the eigenvector matrix: U^T x of :90)
+  CG_HIP(cg::launch_gemm_f32(false, false, N * Fin, M, M, xs, M, U, M, xhat, M, 1, s));
+  CG_HIP(cg::launch_fourier_mix(xhat, W, N, M, Fin, Fout, Yh, s));
+  // y = Yh U^T (inverse transform, :97)
+  float* yt = Fout > 1 ? reinterpret_cast<float*>(w) : y;
+  CG_HIP(cg::launch_gemm_f32(false, true, N * Fout, M, M, Yh, M, U, M, yt, M, 1, s));
+  if (Fout > 1) CG_HIP(cg::launch_transpose_batched(yt, N, Fout, M, y, s));
+  return ok();
+}
+
+int cg_fourier_backward(int32_t N, int32_t M, int32_t Fin, int32_t Fout, const float* U,
+                        const float* W, const float* xhat, const float* dy, float* dx, float* dW,
+                        void* workspace, size_t ws_bytes, void* stream) {
+  if (!U || !W || !xhat || !dy) return fail(CG_ERR_ARG, "fourier_backward: null pointer");
+  if (!fourier_shape_ok(N, M, Fin, Fout)) return fail(CG_ERR_ARG, "fourier_backward: bad shape");
+  size_t need;
+  fourier_ws(N, M, Fin, Fout, nullptr, &need);
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "fourier_backward workspace too small: %zu < %zu", ws_bytes, need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* w = static_cast<char*>(workspace);
+  const size_t xin = size_t(N) * Fin * M * 4, yout = size_t(N) * Fout * M * 4;
+  const float* dys = dy;
+  if (Fout > 1) {
+    float* dyt = reinterpret_cast<float*>(w);
+    w += al256(yout);
+    CG_HIP(cg::launch_transpose_batched(dy, N, M, Fout, dyt, s));
+    dys = dyt;
+  }
+  float* dYh = reinterpret_cast<float*>(w);
+  w += al256(yout);
+  float* dXh = reinterpret_cast<float*>(w);
+  w += al256(xin);
+  CG_HIP(cg::launch_gemm_f32(false, false, N * Fout, M, M, dys, M, U, M, dYh, M, 1, s));
+  if (dW) CG_HIP(cg::launch_fourier_dw(dYh, xhat, N, M, Fin, Fout, dW, s));
+  if (dx) {
+    CG_HIP(cg::launch_fourier_mix_t(dYh, W, N, M, Fin, Fout, dXh, s));
+    float* dxt = Fin > 1 ? reinterpret_cast<float*>(w) : dx;
+    CG_HIP(cg::launch_gemm_f32(false, true, N * Fin, M, M, dXh, M, U, M, dxt, M, 1, s));
+    if (Fin > 1) CG_HIP(cg::launch_transpose_batched(dxt, N, Fin, M, dx, s));
+  }
+  return ok();
+}
+
 static int check_lstm(int64_t R, int32_t H, int32_t gates) {
   if (R < 1 || H < 1) return fail(CG_ERR_ARG, "lstm: bad shape R=%lld H=%d", (long long)R, H);
   if (R * int64_t(H) * 4 >= (int64_t(1) << 31))

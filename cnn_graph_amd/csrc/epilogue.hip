@@ -3,6 +3,9 @@
 // contraction kernel does not apply them itself:
 //   k_act_fwd   y = act(y + res)              (b1relu of x + x_identity, :256-262)
 //   k_relu_bwd  dz = y > 0 ? dy : 0           (ReLU gradient from its output)
+//   k_bias_act_fwd / k_bias_act_bwd
+//               y = act(x + b) with a per-filter (b1*, :189-193) or per-vertex-
+//               and-filter (b2relu, :195-199) bias; dz = dy * act'(y)
 //   k_mse_*     loss = mean((labels - pred)^2), dpred = 2 (pred - labels) / n
 //               (tf.reduce_mean(tf.square(tf.subtract(labels, logits))),
 //               lib/graph_model.py:255), fixed-order two-stage reduction.
@@ -33,6 +36,35 @@ __global__ __launch_bounds__(256) void k_relu_bwd(const float* __restrict__ dy,
                                                   float* __restrict__ dz, int64_t n) {
   for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
     dz[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+
+// y = act(x + bias[i % blen]) (bias NULL: no add); act 0 none, 1 ReLU, 2 tanh.
+// x and y may alias.
+__global__ __launch_bounds__(256) void k_bias_act_fwd(const float* __restrict__ x,
+                                                      const float* __restrict__ bias, int64_t blen,
+                                                      int act, int64_t n, float* __restrict__ y) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    float v = x[i];
+    if (bias) v = v + bias[i % blen];
+    if (act == 1) v = v > 0.f ? v : 0.f;
+    else if (act == 2) v = tanhf(v);
+    y[i] = v;
+  }
+}
+
+// dz = dy * act'(y) from the forward OUTPUT y (TF ReluGrad / TanhGrad:
+// dy * (1 - y*y)).  dz and dy may alias.
+__global__ __launch_bounds__(256) void k_bias_act_bwd(const float* __restrict__ dy,
+                                                      const float* __restrict__ y, int act,
+                                                      int64_t n, float* __restrict__ dz) {
+#pragma clang fp contract(off)
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    const float g = dy[i];
+    float d = g;
+    if (act == 1) d = y[i] > 0.f ? g : 0.f;
+    else if (act == 2) { const float t = y[i]; d = g * (1.f - t * t); }
+    dz[i] = d;
+  }
 }
 
 // Block z sums (labels - pred)^2 over its contiguous chunk (lanes strided,
@@ -85,6 +117,18 @@ hipError_t launch_act_fwd(float* y, const float* res, int act, int64_t n, hipStr
 
 hipError_t launch_relu_bwd(const float* dy, const float* y, float* dz, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_relu_bwd, dim3(grid1d(n, 256)), dim3(256), 0, s, dy, y, dz, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_bias_act_fwd(const float* x, const float* bias, int64_t blen, int act, int64_t n,
+                               float* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_bias_act_fwd, dim3(grid1d(n, 256)), dim3(256), 0, s, x, bias, blen, act, n, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_bias_act_bwd(const float* dy, const float* y, int act, int64_t n, float* dz,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_bias_act_bwd, dim3(grid1d(n, 256)), dim3(256), 0, s, dy, y, act, n, dz);
   return hipGetLastError();
 }
 

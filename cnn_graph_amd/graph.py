@@ -81,6 +81,31 @@ def lmax(L, normalized=True):
     return scipy.sparse.linalg.eigsh(L, k=1, which="LM", return_eigenvectors=False)[0]
 
 
+def fourier(L, algo="eigh", k=1):
+    """Fourier basis = EVD of the Laplacian (lib/graph.py:148-166): (lamb, U)
+    with eigenvalues ascending and U[:, i] the i-th eigenvector.  Same NumPy /
+    SciPy routines as the reference, so U is the reference's U."""
+    def sort(lamb, U):
+        idx = lamb.argsort()
+        return lamb[idx], U[:, idx]
+
+    if algo == "eig":
+        lamb, U = np.linalg.eig(L.toarray())
+        lamb, U = sort(lamb, U)
+    elif algo == "eigh":
+        lamb, U = np.linalg.eigh(L.toarray())
+    elif algo == "eigs":
+        import scipy.sparse.linalg
+        lamb, U = scipy.sparse.linalg.eigs(L, k=k, which="SM")
+        lamb, U = sort(lamb, U)
+    elif algo == "eigsh":
+        import scipy.sparse.linalg
+        lamb, U = scipy.sparse.linalg.eigsh(L, k=k, which="SM")
+    else:
+        raise ValueError(f"unknown algo {algo!r}")
+    return lamb, U
+
+
 def rescale_L(L, lmax=2):
     """``L~ = L / (lmax/2) - I`` (lib/graph.py:232-238), on a private copy.
 

@@ -6,6 +6,9 @@ or a missing library raises.
 
   cheb_forward / cheb_backward  -- lib/graph_conv.py:144-176 and its TF autodiff
   ChebConv (autograd.Function)  -- what chebyshev5 / cheby_conv call
+  bias_act                      -- b1relu / b1tanh / b2relu, lib/graph_conv.py:178-199
+  matmul                        -- tf.matmul of fc, lib/graph_conv.py:220-226 (MFMA GEMM)
+  fourier_conv                  -- filter_in_fourier, lib/graph_conv.py:83-111
   mpool1, apool1                -- lib/graph_conv.py:201-218
   perm_data                     -- lib/coarsening.py:219-240 (device gather)
   adam_update                   -- lib/graph_model.py:293-298
@@ -417,3 +420,133 @@ def adam_update(param, grad, m, v, step: int, lr=1e-3, beta1=0.9, beta2=0.999, e
             raise ValueError(f"{name} must be contiguous")
     _lib.call("cg_adam_update", _p(param), _p(grad), _p(m), _p(v), param.numel(), float(lr),
               float(beta1), float(beta2), float(eps), int(step), float(grad_scale), _stream(param))
+
+
+# -- bias + activation (lib/graph_conv.py:178-199, fc :220-226) --------------------
+BIAS_ACTS = {"none": _lib.CG_ACT_NONE, "relu": _lib.CG_ACT_RELU, "tanh": _lib.CG_ACT_TANH}
+
+
+class _BiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, act: str):
+        _check_dev("x", x)
+        x = x.contiguous()
+        n = x.numel()
+        blen = 1
+        if bias is not None:
+            _check_dev("bias", bias)
+            bias = bias.contiguous()
+            blen = bias.numel()
+            if n % blen:
+                raise ValueError(f"bias of {blen} elements does not tile x of {n}")
+        y = torch.empty_like(x)
+        _lib.call("cg_bias_act_forward", n, blen, _p(x), _p(bias), BIAS_ACTS[act], _p(y), _stream(x))
+        ctx.save_for_backward(y)
+        ctx.act, ctx.blen, ctx.has_bias = act, blen, bias is not None
+        ctx.bshape = None if bias is None else tuple(bias.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        n = dy.numel()
+        dz = torch.empty_like(dy)
+        db = ws = None
+        nb = 0
+        if ctx.has_bias and ctx.needs_input_grad[1]:
+            db = torch.empty(ctx.bshape, device=dy.device, dtype=torch.float32)
+            b = ctypes.c_size_t()
+            _lib.call("cg_bias_act_workspace_bytes", n, ctx.blen, ctypes.byref(b))
+            nb = b.value
+            ws = torch.empty(max(nb, 1), device=dy.device, dtype=torch.uint8)
+        _lib.call("cg_bias_act_backward", n, ctx.blen, _p(dy), _p(y), BIAS_ACTS[ctx.act], _p(dz), _p(db),
+                  0, _p(ws), nb, _stream(dy))
+        return dz, db, None
+
+
+def bias_act(x, bias=None, act: str = "relu"):
+    """act(x + bias) with bias broadcast over the leading axes (bias [F] or
+    [1,1,F]: one per filter; [1,M,F]: one per vertex and filter)."""
+    return _BiasAct.apply(x, bias, act)
+
+
+# -- plain GEMM on MFMA (the tf.matmul of fc / the Fourier transforms) -----------
+def gemm(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+         out: torch.Tensor | None = None) -> torch.Tensor:
+    """op(a) @ op(b) for 2-D fp32 device tensors (cg_gemm_f32)."""
+    _check_dev("a", a)
+    _check_dev("b", b)
+    a, b = a.contiguous(), b.contiguous()
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    Kb, N = (b.shape[1], b.shape[0]) if trans_b else (b.shape[0], b.shape[1])
+    if K != Kb:
+        raise ValueError(f"gemm: inner dimensions differ ({K} vs {Kb})")
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=torch.float32)
+    _check_out("out", out, (M, N))
+    _lib.call("cg_gemm_f32", int(trans_a), int(trans_b), M, N, K, _p(a), a.shape[1], _p(b), b.shape[1],
+              _p(out), N, _stream(a))
+    return out
+
+
+class _MatMul(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        ctx.save_for_backward(a, b)
+        return gemm(a, b)
+
+    @staticmethod
+    def backward(ctx, dc):
+        a, b = ctx.saved_tensors
+        da = gemm(dc, b, trans_b=True) if ctx.needs_input_grad[0] else None
+        db = gemm(a, dc, trans_a=True) if ctx.needs_input_grad[1] else None
+        return da, db
+
+
+def matmul(a, b):
+    """tf.matmul(a, b) for 2-D operands with its gradient, on the HIP GEMM."""
+    return _MatMul.apply(a, b)
+
+
+# -- Fourier filter (lib/graph_conv.py:83-111) ----------------------------------------
+class _Fourier(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, U):
+        for name, t in (("x", x), ("W", W), ("U", U)):
+            _check_dev(name, t)
+        x, W, U = x.contiguous(), W.contiguous(), U.contiguous()
+        N, M, Fin = (int(s) for s in x.shape)
+        if tuple(W.shape[::2]) != (M, Fin) or tuple(U.shape) != (M, M):
+            raise ValueError(f"fourier: need W [M, Fout, Fin] = [{M}, *, {Fin}] and U [{M}, {M}], "
+                             f"got {tuple(W.shape)} and {tuple(U.shape)}")
+        Fout = int(W.shape[1])
+        fb, bb = ctypes.c_size_t(), ctypes.c_size_t()
+        _lib.call("cg_fourier_workspace_bytes", N, M, Fin, Fout, ctypes.byref(fb), ctypes.byref(bb))
+        xhat = torch.empty((N, Fin, M), device=x.device, dtype=torch.float32)
+        y = torch.empty((N, M, Fout), device=x.device, dtype=torch.float32)
+        ws = torch.empty(max(fb.value, 1), device=x.device, dtype=torch.uint8)
+        _lib.call("cg_fourier_forward", N, M, Fin, Fout, _p(U), _p(W), _p(x), _p(xhat), _p(y), _p(ws),
+                  fb.value, _stream(x))
+        ctx.save_for_backward(xhat, W, U)
+        ctx.shape, ctx.bwd_bytes = (N, M, Fin, Fout), bb.value
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xhat, W, U = ctx.saved_tensors
+        N, M, Fin, Fout = ctx.shape
+        dy = dy.contiguous()
+        dx = torch.empty((N, M, Fin), device=dy.device, dtype=torch.float32) \
+            if ctx.needs_input_grad[0] else None
+        dW = torch.empty_like(W) if ctx.needs_input_grad[1] else None
+        ws = torch.empty(max(ctx.bwd_bytes, 1), device=dy.device, dtype=torch.uint8)
+        _lib.call("cg_fourier_backward", N, M, Fin, Fout, _p(U), _p(W), _p(xhat), _p(dy), _p(dx), _p(dW),
+                  _p(ws), ctx.bwd_bytes, _stream(dy))
+        return dx, dW, None
+
+
+def fourier_conv(x, W, U):
+    """filter_in_fourier (lib/graph_conv.py:83-99): x [N, M, Fin], W [M, Fout,
+    Fin], U [M, M] (eigenvectors in columns, device fp32) -> [N, M, Fout]."""
+    return _Fourier.apply(x, W, U)

@@ -118,7 +118,7 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
  * the filter's input gradient into dx (dx += ...) -- the gradient sum of a
  * tensor that feeds both a filter and a residual branch.
  * ------------------------------------------------------------------------- */
-enum { CG_ACT_NONE = 0, CG_ACT_RELU = 1 };
+enum { CG_ACT_NONE = 0, CG_ACT_RELU = 1, CG_ACT_TANH = 2 /* bias_act only */ };
 int cg_cheb_forward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                        const float* x, const float* W, const float* residual, int32_t act,
                        float* basis, float* y, void* workspace, size_t ws_bytes, void* stream);
@@ -147,6 +147,47 @@ int cg_weight_grad(int64_t R, int32_t FinK, int32_t Fout, const float* basis, co
 int cg_bias_grad_workspace_bytes(int64_t R, int32_t C, size_t* bytes);
 int cg_bias_grad(int64_t R, int32_t C, const float* dy, float* db, int32_t accumulate,
                  void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Bias + activation of the GraphConv model (lib/graph_conv.py:178-199):
+ *   y[i] = act(x[i] + bias[i % bias_len])       bias NULL: no add
+ * b1relu / b1tanh: bias_len = F (one bias per filter, [1,1,F]); b2relu:
+ * bias_len = M*F ([1,M,F]); fc (:220-226): bias_len = Mout.  act is
+ * CG_ACT_NONE / RELU / TANH; x and y may alias.  n % bias_len == 0.
+ * Backward: dz = dy * act'(y) from the forward OUTPUT y (TF ReluGrad /
+ * TanhGrad: dy (1 - y^2)); db (+)= column sums of dz viewed [n/bias_len][bias_len]
+ * (fixed order; NULL to skip).  dz and dy may alias.
+ * ------------------------------------------------------------------------- */
+int cg_bias_act_forward(int64_t n, int32_t bias_len, const float* x, const float* bias,
+                        int32_t act, float* y, void* stream);
+int cg_bias_act_workspace_bytes(int64_t n, int32_t bias_len, size_t* bytes);
+int cg_bias_act_backward(int64_t n, int32_t bias_len, const float* dy, const float* y, int32_t act,
+                         float* dz, float* db, int32_t accumulate, void* workspace,
+                         size_t ws_bytes, void* stream);
+/* C[M][N] = op(A) op(B), fp32 on MFMA (v_mfma_f32_32x32x2_f32), row-major with
+ * leading dimensions; trans_a: A stored [K][lda], trans_b: B stored [N][ldb].
+ * The tf.matmul of fc (lib/graph_conv.py:225) and of the Fourier transforms. */
+int cg_gemm_f32(int32_t trans_a, int32_t trans_b, int32_t M, int32_t N, int32_t K, const float* A,
+                int32_t lda, const float* B, int32_t ldb, float* C, int32_t ldc, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Fourier (spectral) filter, lib/graph_conv.py:83-111 (filter_in_fourier,
+ * fourier; lib/models.py:129-159; lib/filter.py fourier_conv):
+ *   U [M][M] = eigenvectors of L in columns (lib/graph.py:148 fourier(),
+ *              U[j][m] = component j of eigenvector m), resident on device
+ *   W [M][Fout][Fin] (the reference's _weight_variable([M, Fout, Fin]))
+ *   x [N][M][Fin] -> y [N][M][Fout]:  y_n = U (W . (U^T x_n)) per frequency
+ * xhat [N][Fin][M] receives U^T x (kept for the backward, which returns
+ * dx = U W^T U^T dy-style gradients and dW[m][fo][fin] = sum_n dYh xhat,
+ * fixed order over n).  dx / dW may be NULL. */
+int cg_fourier_workspace_bytes(int32_t N, int32_t M, int32_t Fin, int32_t Fout, size_t* fwd_bytes,
+                               size_t* bwd_bytes);
+int cg_fourier_forward(int32_t N, int32_t M, int32_t Fin, int32_t Fout, const float* U,
+                       const float* W, const float* x, float* xhat, float* y, void* workspace,
+                       size_t ws_bytes, void* stream);
+int cg_fourier_backward(int32_t N, int32_t M, int32_t Fin, int32_t Fout, const float* U,
+                        const float* W, const float* xhat, const float* dy, float* dx, float* dW,
+                        void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * gconv-LSTM cell pointwise part (lib/gconv_lstm.py:77-221, GConvLSTMCell).
