@@ -167,6 +167,7 @@ struct Fwd {
   int mb[MT];  // byte offsets of the records of this lane's MFMA tile rows
   bool keep_basis;
   Row r;
+  V t1, t2;  // T_{k-1}, T_{k-2} of the own row
   f32x16 acc[MT][NT];
 
   __device__ Fwd(const FastFwdArgs& a, char* smem, int tid) : A(a) {
@@ -222,11 +223,18 @@ struct Fwd {
   template <int L, int CUR, int PRV, int PRV2>
   __device__ __forceinline__ void step(int k) {
 #pragma clang fp contract(off)
-    const V p = lds_v<FV>(ring + r.rr + PRV2 * 4 * FV);  // issued with the gathers
     const V a = r.template dot<FV, L, PRV>(ring);
-    const V o = (k == 1) ? a : rec2(a, p);
+    V o;
+    if (A.dbg & 32) {  // A/B switch: T_{k-2} of the own row re-read from the ring
+      const V p = lds_v<FV>(ring + r.rr + PRV2 * 4 * FV);
+      o = (k == 1) ? a : rec2(a, p);
+    } else {           // T_{k-2} of the own row kept in registers (this thread wrote it)
+      o = (k == 1) ? a : rec2(a, t2);
+    }
     lds_stv<FV>(ring + r.rb + CUR * 4 * FV, o);
     lds_stv<FV>(ring + r.rb1 + CUR * 4 * FV, o);
+    t2 = t1;
+    t1 = o;
     __syncthreads();
   }
 
@@ -273,6 +281,13 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
   }
   for (int i = tid; i < 32 * 3 * FV; i += kT)  // the 32 zero records
     reinterpret_cast<float*>(smem + A.E.zpos * REC)[i] = 0.f;
+  // T_0 of the own row for the register-held T_{k-2}
+  c.t1 = vzero<typename F::V>();
+  if (c.r.row >= 0) {
+#pragma unroll
+    for (int fin = 0; fin < FV; ++fin) setc(c.t1, fin, xn[c.r.row * FV + fin]);
+  }
+  c.t2 = c.t1;
 #pragma unroll
   for (int t = 0; t < F::MT; ++t)
 #pragma unroll
@@ -346,6 +361,7 @@ struct Bwd {
   Row r;
   // fused dW: this wave's basis rows [dm0, dm1), 2 per MFMA
   int dm0, dm1, npair, nexti;
+  V g1, g2;  // G_{k+1}, G_{k+2} of the own row
   f32x16 dacc;
   float da[3][NU], db[3][NU];
 
@@ -397,9 +413,11 @@ struct Bwd {
       dw_load(BUF, (i + 3) * NU);
     }
     const float c = (k >= 1) ? 2.f : 1.f;
-    const V p = lds_v<FV>(ring + r.rr + NX2 * 4 * FV);  // issued with the gathers
     V a = vzero<V>();
     if (i >= 1) a = r.template dot<FV, L, NX1>(ring);
+    // G_{k+2} of the own row: kept in registers (this thread wrote it two
+    // steps ago); debug bit 32 re-reads it from the ring (A/B switch)
+    const V p = (A.dbg & 32) ? lds_v<FV>(ring + r.rr + NX2 * 4 * FV) : g2;
     const int rr = r.row < 0 ? 0 : r.row;
     V g;
 #pragma unroll
@@ -417,6 +435,8 @@ struct Bwd {
     } else {
       lds_stv<FV>(ring + r.rb + CUR * 4 * FV, g);
       lds_stv<FV>(ring + r.rb1 + CUR * 4 * FV, g);
+      g2 = g1;
+      g1 = g;
       __syncthreads();
     }
   }
@@ -528,6 +548,8 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
   // whose dy tiles occupy 32 registers per lane until then
   const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[wave]);
   c.r.template load<FV>(A.E, tid, wl);
+  c.g1 = vzero<typename B::V>();
+  c.g2 = c.g1;
   if (DW) {
     // rows of this wave: 16 near-equal even-sized chunks of [0, M)
     const int q = ((M + 2 * kW - 1) / (2 * kW)) * 2;

@@ -21,9 +21,10 @@ from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 # raw cg_debug_set_flags values: bits 0-7 forward kernel, 8-15 backward kernel,
 # 22 skip dW, 23 skip slab reduce, 24 classic resident kernels, 25 no fused dW
 FWD = {"full": 0, "no_basis_store": 2, "no_mfma": 4, "no_y_store": 8, "no_stores": 2 | 8,
-       "only_spmm": 2 | 4 | 8, "prologue": 16, "classic": 1 << 24}
+       "only_spmm": 2 | 4 | 8, "prologue": 16, "classic": 1 << 24, "ring_tkm2": 32}
 BWD = {"full": 0, "no_phaseA": 2 << 8, "prologue": 16 << 8, "no_fused_dw": 1 << 25,
-       "no_dw": (1 << 25) | (1 << 22), "no_reduce": 1 << 23, "classic": 1 << 24}
+       "no_dw": (1 << 25) | (1 << 22), "no_reduce": 1 << 23, "classic": 1 << 24,
+       "ring_gkp2": 32 << 8}
 
 
 def main():
