@@ -8,7 +8,8 @@ filter on synthetic data already resident in HBM:
     forward  (basis + y = basis W)                     -> cg_cheb_forward
     backward (dx, dW) with a fixed N(0,1) upstream dy   -> cg_cheb_backward
     all-reduce(sum) of dW over ranks (RCCL), N>1 only
-    Adam update of W (TF-1.x rule, grad scaled by 1/world) -> cg_adam_update
+    Adam update of W (TF-1.x rule, grad scaled by 1/world) -> cg_adam_update, or at
+    one GPU (no exchange) fused into the dW reduction     -> cg_cheb_backward_adam
 Weak scaling: every rank processes its own batch of 256 (the batch dimension
 is sharded; L~ and W are replicated -- SURVEY.md §8e).
 
@@ -146,6 +147,8 @@ def main():
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "torch"],
                     help="rccl: cg_allreduce_sum_f32 on the compute stream (default); "
                          "torch: dist.all_reduce (ProcessGroupNCCL, internal stream + events)")
+    ap.add_argument("--unfused-adam", action="store_true",
+                    help="separate cg_adam_update launch even with no exchange step (ablation)")
     ap.add_argument("--force-allreduce", action="store_true",
                     help="run the gradient exchange even at N=1 (1-rank RCCL; overhead study)")
     args = ap.parse_args()
@@ -185,8 +188,16 @@ def main():
         ar_fn = _lib.lib().cg_allreduce_sum_f32
         ar_args = (comm.handle, runner.dW.data_ptr(), runner.dW.numel(), stream)
 
+    # No exchange step (one GPU): the Adam update rides on the dW reduction
+    # (cg_cheb_backward_adam) instead of a separate launch.
+    fuse_adam = not exchange and not args.unfused_adam
+
     def step(i):
         runner.forward(x, W, stream=stream)
+        if fuse_adam:
+            runner.backward_adam(dy, W, m_adam, v_adam, i + 1, grad_scale=1.0 / world,
+                                 stream=stream)
+            return
         runner.backward(dy, W, stream=stream)
         if exchange:
             if comm is not None:
@@ -256,7 +267,9 @@ def main():
                                "Fout=32, chebyshev5 fwd+bwd + dW all-reduce + Adam",
                    "batch_per_gpu": N, "global_batch": N * world, "M": M, "nnz": plan.nnz, "K": K,
                    "Fin": Fin, "Fout": Fout, "path": path, "parallelism": f"dp{world}",
-                   "allreduce": (args.allreduce if exchange else None)},
+                   "allreduce": (args.allreduce if exchange else None),
+                   "adam": ("fused into the dW reduction (cg_cheb_backward_adam)" if fuse_adam
+                            else "cg_adam_update")},
         "roofline": {"bound": "hbm", "kernel": kern[dom]["kernel"],
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4),

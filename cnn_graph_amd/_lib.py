@@ -78,6 +78,9 @@ _SIGNATURES = {
     "cg_maxpool_backward": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
     "cg_avgpool_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
     "cg_avgpool_backward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
+    "cg_cheb_backward_adam": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                               _vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                               _c_i32, ctypes.c_float, _vp, _c_sz, _vp], _c_int),
     "cg_adam_update": ([_vp, _vp, _vp, _vp, _c_i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                         ctypes.c_float, _c_i32, ctypes.c_float, _vp], _c_int),
     "cg_comm_unique_id": ([ctypes.c_char_p], _c_int),

@@ -248,5 +248,16 @@ hipError_t launch_avgpool_bwd(const float* dy, int N, int M, int F, int p, float
                               hipStream_t s);
 hipError_t launch_adam(float* param, const float* grad, float* m, float* v, int64_t n, float lr_t,
                        float beta1, float beta2, float eps, float grad_scale, hipStream_t s);
+// One Adam step applied by the slab reduction that produces its gradient.
+struct AdamStep {
+  float* param;
+  float* m;
+  float* v;
+  float lr_t, beta1, beta2, eps, grad_scale;
+};
+// grad[i] = sum_z slab[z][i] in k_reduce_slabs' order (bitwise the same dW),
+// then the k_adam update of element i, in one launch.
+hipError_t launch_reduce_slabs_adam(const float* slab, int nslab, int64_t count, float* grad,
+                                    const AdamStep& a, hipStream_t s);
 
 }  // namespace cg

@@ -628,7 +628,8 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
 
 int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout, const float* dy,
                   const float* basis, const float* W, float* dx, int dx_acc, float* dW,
-                  void* workspace, size_t ws_bytes, void* stream) {
+                  void* workspace, size_t ws_bytes, void* stream,
+                  const cg::AdamStep* adam = nullptr) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
   if (!dy || !basis || !W) return fail(CG_ERR_ARG, "null dy/basis/W");
@@ -730,7 +731,10 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
     CG_HIP(hipEventRecord(plan->ev_join, plan->side));
     CG_HIP(hipStreamWaitEvent(s, plan->ev_join, 0));
   }
-  if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
+  if (adam)  // reduction + optimizer step in one launch (no exchange in between)
+    CG_HIP(cg::launch_reduce_slabs_adam(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, *adam,
+                                        s));
+  else if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
     CG_HIP(cg::launch_reduce_slabs(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, s));
   return ok();
 }
@@ -757,6 +761,27 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
                      const float* dy, const float* basis, const float* W, float* dx, float* dW,
                      void* workspace, size_t ws_bytes, void* stream) {
   return backward_impl(plan, N, Fin, K, Fout, dy, basis, W, dx, 0, dW, workspace, ws_bytes, stream);
+}
+
+int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                          const float* dy, const float* basis, float* W, float* dx, float* dW,
+                          float* m, float* v, float lr, float beta1, float beta2, float eps,
+                          int32_t step, float grad_scale, void* workspace, size_t ws_bytes,
+                          void* stream) {
+  if (!dW || !W || !m || !v || step < 1)
+    return fail(CG_ERR_ARG, "cheb_backward_adam: dW, W, m, v required and step >= 1");
+  cg::AdamStep a{};
+  a.param = W;
+  a.m = m;
+  a.v = v;
+  a.lr_t = float(double(lr) * std::sqrt(1.0 - std::pow(double(beta2), step)) /
+                 (1.0 - std::pow(double(beta1), step)));
+  a.beta1 = beta1;
+  a.beta2 = beta2;
+  a.eps = eps;
+  a.grad_scale = grad_scale;
+  return backward_impl(plan, N, Fin, K, Fout, dy, basis, W, dx, 0, dW, workspace, ws_bytes, stream,
+                       &a);
 }
 
 int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,

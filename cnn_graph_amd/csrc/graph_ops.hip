@@ -105,19 +105,54 @@ __global__ __launch_bounds__(256) void k_avgpool_bwd(const float* __restrict__ d
 
 // m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ; p -= lr_t m / (sqrt(v) + eps)
 // with lr_t = lr sqrt(1-b2^t)/(1-b1^t) computed on the host (TF's ApplyAdam).
+// TF-1.x Adam on one element (lib/graph_model.py:293-298 via tf.train.AdamOptimizer);
+// shared by k_adam and k_reduce_slabs_adam so both round identically.
+__device__ __forceinline__ void adam_elem(float* __restrict__ param, float* __restrict__ m,
+                                          float* __restrict__ v, int64_t i, float grad,
+                                          float grad_scale, float lr_t, float beta1, float beta2,
+                                          float eps) {
+  const float g = grad * grad_scale;
+  const float mi = m[i] + (g - m[i]) * (1.f - beta1);
+  const float vi = v[i] + (g * g - v[i]) * (1.f - beta2);
+  m[i] = mi;
+  v[i] = vi;
+  param[i] = param[i] - lr_t * mi / (sqrtf(vi) + eps);
+}
+
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ param,
                                               const float* __restrict__ grad, float* __restrict__ m,
                                               float* __restrict__ v, int64_t n, float lr_t,
                                               float beta1, float beta2, float eps,
                                               float grad_scale) {
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += int64_t(gridDim.x) * blockDim.x) {
-    const float g = grad[i] * grad_scale;
-    const float mi = m[i] + (g - m[i]) * (1.f - beta1);
-    const float vi = v[i] + (g * g - v[i]) * (1.f - beta2);
-    m[i] = mi;
-    v[i] = vi;
-    param[i] = param[i] - lr_t * mi / (sqrtf(vi) + eps);
+       i += int64_t(gridDim.x) * blockDim.x)
+    adam_elem(param, m, v, i, grad[i], grad_scale, lr_t, beta1, beta2, eps);
+}
+
+// Slab reduction + Adam for a step with no exchange between them (one GPU):
+// the summation is k_reduce_slabs' (wave w sums slabs w, w+16, ..., then the 16
+// partials in wave order), so grad is bitwise the unfused dW; wave 0 then
+// applies the update.  Saves the separate k_adam launch (~5 us, dispatch-bound).
+__global__ __launch_bounds__(1024) void k_reduce_slabs_adam(const float* __restrict__ slab,
+                                                            int nslab, int64_t count,
+                                                            float* __restrict__ grad,
+                                                            AdamStep a) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t i = int64_t(blockIdx.x) * 64 + lane;
+  float s = 0.f;
+  if (i < count) {
+#pragma unroll 8
+    for (int z = w; z < nslab; z += 16) s = s + slab[int64_t(z) * count + i];
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i < count) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t = t + part[q][lane];
+    grad[i] = t;
+    adam_elem(a.param, a.m, a.v, i, t, a.grad_scale, a.lr_t, a.beta1, a.beta2, a.eps);
   }
 }
 
@@ -166,6 +201,13 @@ hipError_t launch_adam(float* param, const float* grad, float* m, float* v, int6
                        float beta1, float beta2, float eps, float grad_scale, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3(grid_for(n, 256)), dim3(256), 0, s, param, grad, m, v, n, lr_t,
                      beta1, beta2, eps, grad_scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_slabs_adam(const float* slab, int nslab, int64_t count, float* grad,
+                                    const AdamStep& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_slabs_adam, dim3(unsigned((count + 63) / 64)), dim3(1024), 0, s, slab,
+                     nslab, count, grad, a);
   return hipGetLastError();
 }
 

@@ -199,6 +199,23 @@ class ChebRunner:
         _lib.check("cg_cheb_backward", st)
         return (self.dx if need_dx else None), self.dW
 
+    def backward_adam(self, dy: torch.Tensor, W: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
+                      step: int, lr: float = 1e-3, beta1: float = 0.9, beta2: float = 0.999,
+                      eps: float = 1e-8, grad_scale: float = 1.0, need_dx: bool = True,
+                      stream=None):
+        """backward + Adam on W in place, the update fused into the dW reduction
+        (cg_cheb_backward_adam; one-GPU step, lib/graph_model.py:277-298)."""
+        for name, t_ in (("W", W), ("m", m), ("v", v)):
+            _check_dev(name, t_)
+        s = stream if stream is not None else torch.cuda.current_stream(dy.device).cuda_stream
+        st = _lib.lib().cg_cheb_backward_adam(
+            self.plan.handle, self.N, self.Fin, self.K, self.Fout, dy.data_ptr(),
+            self.basis.data_ptr(), W.data_ptr(), self.dx.data_ptr() if need_dx else None,
+            self.dW.data_ptr(), m.data_ptr(), v.data_ptr(), lr, beta1, beta2, eps, step,
+            grad_scale, self.bws.data_ptr(), self.bwd_bytes, s)
+        _lib.check("cg_cheb_backward_adam", st)
+        return (self.dx if need_dx else None), self.dW
+
 
 class ChebConv(torch.autograd.Function):
     """y = chebyshev5(x; L~, W, K) with the HIP forward/backward kernels."""

@@ -246,6 +246,18 @@ int cg_adam_update(float* param, const float* grad, float* m, float* v, int64_t 
                    float beta1, float beta2, float eps, int32_t step, float grad_scale,
                    void* stream);
 
+/* cg_cheb_backward followed by cg_adam_update(W, dW, m, v, ...) with the
+ * optimizer step applied by the dW reduction itself -- for a training step
+ * with no gradient exchange between them (one GPU; lib/graph_model.py:277-298,
+ * `optimizer.minimize` = compute_gradients + apply_gradients).  dW receives the
+ * same (bitwise) gradient as cg_cheb_backward; W, m, v are updated in place
+ * after every read of W by the backward (stream order).  dW, W, m, v required. */
+int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                          const float* dy, const float* basis, float* W, float* dx, float* dW,
+                          float* m, float* v, float lr, float beta1, float beta2, float eps,
+                          int32_t step, float grad_scale, void* workspace, size_t ws_bytes,
+                          void* stream);
+
 /* ---------------------------------------------------------------------------
  * Graph coarsening (host code; no device work).
  * Greedy Graclus matching of one level, lib/coarsening.py:119-165

@@ -1,0 +1,82 @@
+"""cg_cheb_backward_adam: the one-GPU training step's Adam update applied by the
+dW slab reduction (lib/graph_model.py:277-298, compute_gradients +
+apply_gradients with no exchange in between).  Bar: dW (independent of W) bitwise
+equal to cg_cheb_backward every step, dx bitwise at step 1 (same W); W, m, v after three steps equal to cg_cheb_backward +
+cg_adam_update within 1e-6 max-abs-normalised (the two launches may contract
+the Adam arithmetic differently), and the fused W within 1e-5 of the float64
+Adam restatement."""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.sparse
+
+from conftest import case, load_golden
+from oracle import cheb_oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(built_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_graph_amd import _lib
+    _lib.lib()
+    return torch.device("cuda", 0)
+
+
+def adam64(W, g, m, v, step, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
+    """TF-1.x AdamOptimizer update (float64), the rule k_adam implements."""
+    lr_t = lr * np.sqrt(1 - b2 ** step) / (1 - b1 ** step)
+    m = m + (g - m) * (1 - b1)
+    v = v + (g * g - v) * (1 - b2)
+    return W - lr_t * m / (np.sqrt(v) + eps), m, v
+
+
+@pytest.mark.parametrize("name,path", [("golden_A.npz", "resident"), ("golden_B.npz", "resident"),
+                                       ("golden_E.npz", "stream")])
+def test_backward_adam_matches_unfused(dev, name, path):
+    from cnn_graph_amd import _lib, ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden(name))
+    M, N, Fin, K, Fout = c["M"], c["N"], c["Fin"], c["K"], c["Fout"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    plan = ChebPlan(Lt, device=0, path=path)
+    x = torch.from_numpy(np.ascontiguousarray(c["x"], dtype=np.float32)).to(dev)
+    dy = torch.from_numpy(np.ascontiguousarray(c["dy"], dtype=np.float32)).to(dev)
+    W0 = torch.from_numpy(np.ascontiguousarray(c["W"], dtype=np.float32)).to(dev)
+    ra, rb = ops.ChebRunner(plan, N, Fin, K, Fout, dev), ops.ChebRunner(plan, N, Fin, K, Fout, dev)
+    Wa, Wb = W0.clone(), W0.clone()
+    ma, va, mb, vb = (torch.zeros_like(W0) for _ in range(4))
+    adam = _lib.lib().cg_adam_update
+    W64, m64, v64 = (f.astype(np.float64) for f in (c["W"], np.zeros_like(c["W"]), np.zeros_like(c["W"])))
+    for step in (1, 2, 3):
+        ra.forward(x, Wa)
+        rb.forward(x, Wb)
+        dxa, dWa = ra.backward_adam(dy, Wa, ma, va, step)
+        dxb, dWb = rb.backward(dy, Wb)
+        torch.cuda.synchronize()
+        assert torch.equal(dWa, dWb), "fused reduction changed dW"
+        if step == 1:  # same W: bitwise; later W differs by Adam rounding only
+            assert torch.equal(dxa, dxb)
+        else:
+            assert O.normwise_err(dxa.cpu().numpy(), dxb.cpu().numpy()) < 1e-5
+        g64 = dWb.cpu().numpy().astype(np.float64)
+        _lib.check("cg_adam_update", adam(Wb.data_ptr(), dWb.data_ptr(), mb.data_ptr(), vb.data_ptr(),
+                                          Wb.numel(), ctypes.c_float(1e-3), ctypes.c_float(0.9),
+                                          ctypes.c_float(0.999), ctypes.c_float(1e-8), step,
+                                          ctypes.c_float(1.0), None))
+        W64, m64, v64 = adam64(W64, g64, m64, v64, step)
+        torch.cuda.synchronize()
+        for a, b in ((Wa, Wb), (ma, mb), (va, vb)):
+            assert O.normwise_err(a.cpu().numpy(), b.cpu().numpy()) < 1e-6
+        assert O.normwise_err(Wa.cpu().numpy(), W64) < 1e-5
+
+
+def test_backward_adam_rejects_missing_state(dev):
+    from cnn_graph_amd import _lib
+    st = _lib.lib().cg_cheb_backward_adam(None, 1, 1, 2, 1, None, None, None, None, None, None, None,
+                                           1e-3, 0.9, 0.999, 1e-8, 1, 1.0, None, 0, None)
+    assert st != 0
