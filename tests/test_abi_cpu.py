@@ -51,6 +51,9 @@ def test_null_and_shape_errors(built_lib):
     assert h.cg_cheb_forward(None, 1, 1, 1, 1, None, None, None, None, None, 0, None) == _lib.CG_ERR_ARG
     assert h.cg_maxpool_forward(None, 1, 6, 1, 4, None, None, None) == _lib.CG_ERR_ARG
     assert h.cg_adam_update(None, None, None, None, 1, 0.1, 0.9, 0.999, 1e-8, 0, 1.0, None) == _lib.CG_ERR_ARG
+    assert h.cg_cheb_backward_adam(None, 1, 1, 2, 1, None, None, None, None, None, None, None,
+                                   1e-3, 0.9, 0.999, 1e-8, 1, 1.0, None, 0, None) == _lib.CG_ERR_ARG
+    assert "backward_adam" in h.cg_last_error().decode()
     with pytest.raises(_lib.CGError):
         _lib.call("cg_plan_set_path", None, 0)
 

@@ -74,9 +74,3 @@ def test_backward_adam_matches_unfused(dev, name, path):
             assert O.normwise_err(a.cpu().numpy(), b.cpu().numpy()) < 1e-6
         assert O.normwise_err(Wa.cpu().numpy(), W64) < 1e-5
 
-
-def test_backward_adam_rejects_missing_state(dev):
-    from cnn_graph_amd import _lib
-    st = _lib.lib().cg_cheb_backward_adam(None, 1, 1, 2, 1, None, None, None, None, None, None, None,
-                                           1e-3, 0.9, 0.999, 1e-8, 1, 1.0, None, 0, None)
-    assert st != 0
