@@ -21,11 +21,19 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%
 	$(HIPCC) $(CXXFLAGS) -MMD -MP -c $< -o $@
 
 $(LIB): $(OBJS)
+	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 -include $(DEPS)
 
-clean:
-	rm -rf build $(LIB)
+# Ablation build (scripts/ablate.py, via CG_LIB_PATH): the same sources with
+# -DCG_DEBUG, which compiles in cg_debug_set_flags and the kernels' timing
+# switches.  Never loaded by the package, the tests or the bench.
+DEBUG_LIB ?= scripts/_debug/libcheb_mi355_debug.so
+debug:
+	$(MAKE) OBJ_DIR=build/dobj LIB=$(DEBUG_LIB) EXTRA=-DCG_DEBUG all
 
-.PHONY: all clean
+clean:
+	rm -rf build $(LIB) $(DEBUG_LIB)
+
+.PHONY: all clean debug

@@ -10,8 +10,10 @@ filter on synthetic data already resident in HBM:
     all-reduce(sum) of dW over ranks (RCCL), N>1 only
     Adam update of W (TF-1.x rule, grad scaled by 1/world) -> cg_adam_update, or at
     one GPU (no exchange) fused into the dW reduction     -> cg_cheb_backward_adam
-Weak scaling: every rank processes its own batch of 256 (the batch dimension
-is sharded; L~ and W are replicated -- SURVEY.md §8e).
+Weak scaling (default): every rank processes its own batch of 256 (the batch
+dimension is sharded; L~ and W are replicated -- SURVEY.md §8e).  Strong
+scaling: --global-batch G fixes the whole job's batch and shards it over the
+ranks (lib/graph_model.py:296-298 is where the exchange sits in the reference).
 
 The timed loop issues exactly those C-ABI calls on torch's current stream
 (ctypes, pre-bound arguments, no per-step allocation or event), bracketed by
@@ -22,8 +24,11 @@ live under profiles/ (scripts/prof_pmc.sh), whose PMC-measured HBM bytes of
 the dominant kernel are reported as roofline.traffic when they match this
 configuration.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
-        (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch G]
+  N > 1 under torchrun (python -m torch.distributed.run --nproc-per-node N ...
+  bench.py --gpus N): one rank per GPU, WORLD_SIZE must equal N.  N > 1
+  without torchrun: bench.py starts that torchrun itself as a child process
+  (before anything touches the GPU) and exits with its status.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -31,7 +36,10 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -72,15 +80,46 @@ def algorithmic_bytes(M, nnz, B, K):
     return fwd, bwd, csr
 
 
-def cpu_baseline(L, fake, K, Fout, seconds=12.0, threads=16):
-    """The oracle (tests-only CPU restatement, scipy SpMM + numpy GEMM) timed on
-    a bounded sample of the same workload: batches of 32 samples, fwd+bwd."""
+def host_cpus():
+    """(usable CPUs, affinity CPUs, cgroup quota or None, os.cpu_count()): the
+    CPUs this process may actually run on -- the box's CPU share, not the
+    machine's core count that os.cpu_count() reports."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    return usable, aff, quota, os.cpu_count()
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(L, fake, K, Fout, n=256, seconds=10.0):
+    """The oracle (tests-only CPU restatement: scipy SpMM in the reference's
+    order + numpy/BLAS GEMMs and layout transposes, fp32) timed on the SAME
+    workload as the GPU line -- config B, batch 256, fwd+bwd -- for a bounded
+    number of repetitions (>= 1, until ~`seconds`), BLAS on every CPU this
+    process may use (the scipy SpMM itself is single-threaded, as TF's CPU
+    SparseTensorDenseMatMul functor the survey describes)."""
     from threadpoolctl import threadpool_limits
     from oracle import cheb_oracle as O
     from cnn_graph_amd.graph import rescale_L, canonical_csr
     rp, ci, v = canonical_csr(rescale_L(L, 2))
     M = L.shape[0]
-    n = 32
+    threads, aff, quota, ncpu = host_cpus()
     rng = np.random.default_rng(1)
     x = rng.random((n, M, 1), dtype=np.float32)
     x[:, fake, :] = 0
@@ -96,10 +135,13 @@ def cpu_baseline(L, fake, K, Fout, seconds=12.0, threads=16):
             el = time.perf_counter() - t0
             if el > seconds:
                 break
+    q = "none" if quota is None else f"{quota:g}"
     return {"value": round(reps * n / el, 1), "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} fwd+bwd passes of a 32-sample batch of config B (oracle/cheb_oracle.py, "
-                      f"fp32, scipy SpMM single-threaded + numpy BLAS with {threads} threads), {el:.1f}s; "
-                      f"host has {os.cpu_count()} logical CPUs"}
+            "cpu_model": cpu_model(),
+            "sample": f"{reps} fwd+bwd passes of the full config-B batch (N={n}, M={M}, K={K}, "
+                      f"Fout={Fout}; oracle/cheb_oracle.py, fp32) in {el:.1f}s; BLAS threads = "
+                      f"{threads} = the CPUs this process may use (affinity {aff}, cgroup quota {q}; "
+                      f"os.cpu_count() = {ncpu} is the whole machine); scipy SpMM single-threaded"}
 
 
 def burst_ms(fn, reps=50, rounds=5):
@@ -135,15 +177,30 @@ def pmc_traffic(kernel, cfg):
     return int(c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024), d.get("source")
 
 
+def spawn_ranks(n):
+    """Re-launch this command under torchrun with n ranks (one per GPU) as a
+    CHILD process -- nothing here has touched the GPU -- and return its status."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=256, help="samples per GPU")
+    ap.add_argument("--batch", type=int, default=256, help="samples per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="fixed whole-job batch sharded over the ranks (strong scaling)")
     ap.add_argument("--path", default="auto", choices=["auto", "resident", "stream"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "torch"],
                     help="rccl: cg_allreduce_sum_f32 on the compute stream (default); "
                          "torch: dist.all_reduce (ProcessGroupNCCL, internal stream + events)")
@@ -153,6 +210,11 @@ def main():
                     help="run the gradient exchange even at N=1 (1-rank RCCL; overhead study)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
     rank, world, local = cdist.init()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -160,7 +222,15 @@ def main():
     K, Fin, Fout = 25, 1, 32
     L, fake = load_config_b()
     M = L.shape[0]
-    N = args.batch
+    strong = args.global_batch is not None
+    if strong:
+        lo, hi = cdist.shard(args.global_batch, rank, world)
+        N = hi - lo
+        if N < 1:
+            sys.exit(f"bench.py: global batch {args.global_batch} < {world} ranks")
+    else:
+        N = args.batch
+    N_global = args.global_batch if strong else N * world
     plan = ChebPlan.from_laplacian(L, lmax=2, device=local, path=args.path)
     path = plan.query_path(N, Fin, K, Fout)
 
@@ -246,9 +316,11 @@ def main():
     ach = kern[dom]["alg_bytes"] / (kern[dom]["ms"] * 1e-3) / 1e9
     cfg_key = {"M": M, "N": N, "K": K, "Fin": Fin, "Fout": Fout}
     traffic, traffic_src = pmc_traffic(kern[dom]["kernel"].split("+")[0], cfg_key)
+    fwd_traffic, _ = pmc_traffic(fwd_kernel, cfg_key)
     contraction_tflops = 2.0 * N * M * Fin * K * Fout / (fwd_ms * 1e-3) / 1e12
+    spmm_ach = bytes_fwd / (fwd_ms * 1e-3) / 1e9
 
-    value = N * world * args.steps / elapsed
+    value = N_global * args.steps / elapsed
     out = {
         "metric": "Chebyshev-K fwd+bwd samples/sec",
         "value": round(value, 1),
@@ -258,14 +330,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (x~U[0,1) with fake vertices 0, dy~N(0,1), W~truncnorm(0,0.1)); "
                 "graph = reference MNIST recipe M=976",
         "config": {"workload": "config B: MNIST 8-NN grid coarsened, M=976, nnz=6396, K=25, Fin=1, "
                                "Fout=32, chebyshev5 fwd+bwd + dW all-reduce + Adam",
-                   "batch_per_gpu": N, "global_batch": N * world, "M": M, "nnz": plan.nnz, "K": K,
+                   "batch_per_gpu": N, "global_batch": N_global, "M": M, "nnz": plan.nnz, "K": K,
                    "Fin": Fin, "Fout": Fout, "path": path, "parallelism": f"dp{world}",
                    "allreduce": (args.allreduce if exchange else None),
                    "adam": ("fused into the dW reduction (cg_cheb_backward_adam)" if fuse_adam
@@ -278,6 +350,14 @@ def main():
                      "avg_launch_ms": round(kern[dom]["ms"], 5),
                      "timing": "HIP events on the launch stream around 50 back-to-back launches",
                      "traffic_source": traffic_src},
+        # BASELINE.json's north-star target: >= 40 % of the HBM roofline on the
+        # K-step CSR SpMM of config B, i.e. the forward basis kernel (the
+        # headline `roofline` above is the slowest kernel of the step)
+        "roofline_spmm_fwd": {"bound": "hbm", "kernel": fwd_kernel, "achieved": round(spmm_ach, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(spmm_ach / HBM_PEAK_GBS, 4), "target_frac": 0.40,
+                              "traffic": fwd_traffic, "alg_bytes_per_launch": bytes_fwd,
+                              "avg_launch_ms": round(fwd_ms, 5)},
         "kernels": {k: {"kernel": v["kernel"], "avg_ms": round(v["ms"], 5), "alg_bytes": v["alg_bytes"],
                         "alg_GBps": round(v["alg_bytes"] / (v["ms"] * 1e-3) / 1e9, 1)}
                     for k, v in kern.items()},

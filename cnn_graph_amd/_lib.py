@@ -18,6 +18,9 @@ CG_OK, CG_ERR_ARG, CG_ERR_HIP, CG_ERR_UNSUPPORTED, CG_ERR_ALLOC, CG_ERR_COMM = r
 CG_PATH_AUTO, CG_PATH_RESIDENT, CG_PATH_STREAM = 0, 1, 2
 CG_ACT_NONE, CG_ACT_RELU, CG_ACT_TANH = 0, 1, 2
 PATHS = {"auto": CG_PATH_AUTO, "resident": CG_PATH_RESIDENT, "stream": CG_PATH_STREAM}
+CG_VARIANT_AUTO, CG_VARIANT_CLASSIC, CG_VARIANT_UNFUSED_DW = 0, 1, 2
+VARIANTS = {"auto": CG_VARIANT_AUTO, "classic": CG_VARIANT_CLASSIC,
+            "unfused_dw": CG_VARIANT_UNFUSED_DW}
 
 
 class CGError(RuntimeError):
@@ -40,6 +43,7 @@ _SIGNATURES = {
                         _ip32, _ip32, _fp32], _c_int),
     "cg_plan_destroy": ([_vp], _c_int),
     "cg_plan_set_path": ([_vp, _c_int], _c_int),
+    "cg_plan_set_variant": ([_vp, _c_int], _c_int),
     "cg_plan_query_path": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_int)], _c_int),
     "cg_cheb_workspace_bytes": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_sz),
                                  ctypes.POINTER(_c_sz)], _c_int),

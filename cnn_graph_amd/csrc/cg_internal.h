@@ -21,9 +21,19 @@ constexpr int kLdsBytes = 160 * 1024;  // gfx950 LDS per CU
 __host__ __device__ inline int lds_vertex_stride(int M) { return ((M + 31) / 32) * 32 + 1; }
 __host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
-// Ablation switches for timing experiments only (never set in production):
-// bits 0-7 forward resident kernel, bits 8-15 backward.  See cg_debug_set_flags.
+// Timing-ablation switches (bits 0-7 forward resident kernel, 8-15 backward,
+// 22 skip dW, 23 skip the slab reduction; outputs are WRONG when set).  They
+// exist only in the ablation build (`make debug`, -DCG_DEBUG, a separate .so
+// that scripts/ablate.py loads through CG_LIB_PATH): in the release library
+// there is no such state and every CG_DBG test folds to false at compile time.
+#ifdef CG_DEBUG
 extern int g_debug_flags;
+#define CG_DBG(flags, bit) (((flags) & (bit)) != 0)
+inline int debug_flags() { return g_debug_flags; }
+#else
+#define CG_DBG(flags, bit) false
+constexpr int debug_flags() { return 0; }
+#endif
 
 // ---- resident (LDS) path ---------------------------------------------------
 struct ResidentGeom {

@@ -15,9 +15,11 @@
 
 #include "cg_internal.h"
 
+#ifdef CG_DEBUG
 namespace cg {
 int g_debug_flags = 0;
 }
+#endif
 
 struct cg_plan {
   int device = 0;
@@ -25,6 +27,7 @@ struct cg_plan {
   int64_t nnz = 0, nnzT = 0;
   int max_row_nnz = 0, max_row_nnzT = 0;
   int path = CG_PATH_AUTO;
+  int variant = CG_VARIANT_AUTO;
   int* rowptr = nullptr;
   int* col = nullptr;
   float* val = nullptr;
@@ -36,8 +39,6 @@ struct cg_plan {
   // lengths; null when the row lengths are near-uniform
   int* rperm = nullptr;
   int* trperm = nullptr;
-  hipStream_t side = nullptr;  // dW kernel runs here, overlapped with the dx recurrence
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // thread-slot images of L~ and L~^T for the resident kernels (M <= 2048)
   struct Slots {
     int* buf = nullptr;  // one allocation: row | len | beg | col | val | wlen
@@ -256,9 +257,6 @@ void free_plan(cg_plan* p) {
   if (p->tslots.buf) (void)hipFree(p->tslots.buf);
   if (p->fast.buf) (void)hipFree(p->fast.buf);
   if (p->tfast.buf) (void)hipFree(p->tfast.buf);
-  if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
-  if (p->ev_join) (void)hipEventDestroy(p->ev_join);
-  if (p->side) (void)hipStreamDestroy(p->side);
   delete p;
 }
 
@@ -280,14 +278,15 @@ int check_shape(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fou
   return CG_OK;
 }
 
-// Debug bit 24 forces the classic resident kernels (cheb_resident.hip) where
-// the fast ones (cheb_fast.hip) would run; bit 25 disables the fused dW.
+// CG_VARIANT_CLASSIC runs the classic resident kernels (cheb_resident.hip)
+// where the fast ones (cheb_fast.hip) would; CG_VARIANT_UNFUSED_DW keeps the
+// fast kernels but computes dW with the separate streaming GEMM.
 cg::FastGeom fast_geom(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout) {
   return cg::fast_geometry(p->M, p->fast.view.P, p->max_row_nnz, p->max_row_nnzT, Fin, K, Fout);
 }
 
 bool use_fast(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool backward) {
-  if (cg::g_debug_flags & (1 << 24)) return false;
+  if (p->variant == CG_VARIANT_CLASSIC) return false;
   if (!(backward ? p->tfast.ok : p->fast.ok)) return false;
   const cg::FastGeom g = fast_geom(p, Fin, K, Fout);
   return backward ? g.bwd_ok : g.fwd_ok;
@@ -295,7 +294,7 @@ bool use_fast(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool backw
 
 bool fused_dw(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout) {
   return use_fast(p, Fin, K, Fout, true) && fast_geom(p, Fin, K, Fout).dw_fused &&
-         !(cg::g_debug_flags & (1 << 25));
+         p->variant != CG_VARIANT_UNFUSED_DW;
 }
 
 int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool backward,
@@ -321,8 +320,7 @@ inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 struct StreamWs {
   size_t slots;  // forward: T_1 .. T_{K-2}, (K-2) * N*M*Fin floats
-  size_t ring;   // backward: G ring, 3 * N*M*Fin floats
-  size_t dA;     // backward: dBasis, N*M*FinK floats (k-major)
+  size_t dA;     // backward: dBasis, N*M*FinK floats (k-major); G_k overwrites plane k
 };
 
 StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout) {
@@ -331,7 +329,6 @@ StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t 
   const int64_t FinK = int64_t(Fin) * K;
   const int64_t NM = int64_t(N) * p->M;
   w.slots = al256(size_t(K > 2 ? K - 2 : 0) * size_t(p->M) * size_t(B) * 4);
-  w.ring = al256(size_t(3) * size_t(p->M) * size_t(B) * 4);
   w.dA = al256(size_t(NM) * size_t(FinK) * 4);
   (void)Fout;
   return w;
@@ -344,8 +341,11 @@ size_t dw_slab_bytes(int64_t R, int32_t N, int FinK, int Fout) {
   return al256(n * size_t(FinK) * size_t(Fout) * 4);
 }
 
-// Workspace layout.  forward: [T ring] (streaming path only).
-// backward: [dW slabs][T ring][dBasis] (the last two for the streaming path).
+// Workspace layout.  forward: [T_1 .. T_{K-2}] (streaming path only).
+// backward: [dW slabs][dBasis] (dBasis for the streaming path only; the
+// reverse recurrence writes G_k over plane k of it, so it needs no ring).
+// The forward's workspace is dead once the forward has returned, so one
+// buffer of max(fwd, bwd) bytes may serve both.
 int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                     size_t* fwd, size_t* bwd) {
   int pf = 0, pb = 0, rc;
@@ -354,17 +354,7 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
   const StreamWs w = stream_ws(p, N, Fin, K, Fout);
   const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, N, Fin * K, Fout);
   *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.slots;
-  *bwd = slabs + ((pb == CG_PATH_RESIDENT) ? 0 : (w.ring + w.dA));
-  return CG_OK;
-}
-
-// Side stream + fork/join events for the dW kernel (created on first use,
-// on the plan's device; never inside graph capture after the first call).
-int ensure_side_stream(cg_plan* p) {
-  if (p->side) return CG_OK;
-  CG_HIP(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
-  CG_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-  CG_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+  *bwd = slabs + ((pb == CG_PATH_RESIDENT) ? 0 : w.dA);
   return CG_OK;
 }
 
@@ -372,13 +362,16 @@ int ensure_side_stream(cg_plan* p) {
 
 extern "C" {
 
-int cg_version(void) { return 200; }
+int cg_version(void) { return 201; }
 
-// Timing-ablation hook (not in the public header; outputs are WRONG when set).
+#ifdef CG_DEBUG
+// Timing-ablation hook of the debug build only (`make debug`; not in the
+// public header, not in the release library; outputs are WRONG when set).
 int cg_debug_set_flags(int flags) {
   cg::g_debug_flags = flags;
   return ok();
 }
+#endif
 
 // Not in the public header: lets comm.cpp report through cg_last_error().
 int cg_internal_set_error(int code, const char* msg) {
@@ -514,6 +507,15 @@ int cg_plan_set_path(cg_plan* plan, int path) {
   return ok();
 }
 
+int cg_plan_set_variant(cg_plan* plan, int variant) {
+  if (!plan) return fail(CG_ERR_ARG, "null plan");
+  if (variant != CG_VARIANT_AUTO && variant != CG_VARIANT_CLASSIC &&
+      variant != CG_VARIANT_UNFUSED_DW)
+    return fail(CG_ERR_ARG, "bad kernel variant %d", variant);
+  plan->variant = variant;
+  return ok();
+}
+
 int cg_plan_query_path(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                        int* path) {
   int rc = check_shape(plan, N, Fin, K, Fout);
@@ -560,7 +562,7 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
     a.Fin = Fin;
     a.K = K;
     a.Fout = Fout;
-    a.dbg = cg::g_debug_flags & 0xff;
+    a.dbg = cg::debug_flags() & 0xff;
     a.E = plan->fast.view;
     a.x = x;
     a.W = y ? W : nullptr;
@@ -579,7 +581,7 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
     a.K = K;
     a.Fout = Fout;
     a.Mp = cg::lds_vertex_stride(M);
-    a.dbg = cg::g_debug_flags & 0xff;
+    a.dbg = cg::debug_flags() & 0xff;
     a.E = plan->slots.view;
     a.col = plan->col;
     a.val = plan->val;
@@ -647,22 +649,12 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   const int64_t R = int64_t(N) * M;
   const int chunks = cg::dw_chunks(R);
 
-  // dW = basis^T dy is HBM-streaming and independent of the (latency-bound)
-  // dx recurrence: fork it onto the plan's side stream so the two overlap on
-  // the same CUs, join before the fixed-order slab reduction.
-  if ((rc = ensure_side_stream(plan))) return rc;
+  // Everything runs on the caller's stream.  (Forking the streaming dW GEMM
+  // onto a side stream to overlap the dx recurrence was measured on MI355X:
+  // the event fork + join costs ~20 us per call, more than the overlap gains.)
   char* base = static_cast<char*>(workspace);
   float* slabs = reinterpret_cast<float*>(base);
   char* rest = base + dw_slab_bytes(R, N, FinK, Fout);
-  // Measured on MI355X: a hipEventRecord/hipStreamWaitEvent fork+join costs
-  // ~20 us per call, far more than the overlap gains, so it is opt-in
-  // (cg_debug_set_flags bit 21) and dW normally runs on the caller's stream.
-  const bool overlap = dx != nullptr && (cg::g_debug_flags & (1 << 21));
-  hipStream_t sdw = overlap ? plan->side : s;
-  if (overlap) {
-    CG_HIP(hipEventRecord(plan->ev_fork, s));
-    CG_HIP(hipStreamWaitEvent(plan->side, plan->ev_fork, 0));
-  }
   const bool fused =
       dx != nullptr && dW != nullptr && path == CG_PATH_RESIDENT && fused_dw(plan, Fin, K, Fout);
   if (dx) {
@@ -674,7 +666,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       a.K = K;
       a.Fout = Fout;
       a.Mp = cg::lds_vertex_stride(M);
-      a.dbg = (cg::g_debug_flags >> 8) & 0xff;
+      a.dbg = (cg::debug_flags() >> 8) & 0xff;
       a.dscratch_bytes = g.dscratch;
       a.E = plan->tfast.view;
       a.dy = dy;
@@ -693,7 +685,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       a.K = K;
       a.Fout = Fout;
       a.Mp = cg::lds_vertex_stride(M);
-      a.dbg = (cg::g_debug_flags >> 8) & 0xff;
+      a.dbg = (cg::debug_flags() >> 8) & 0xff;
       a.E = plan->tslots.view;
       a.col = plan->tcol;
       a.val = plan->tval;
@@ -703,12 +695,14 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       a.dx_acc = dx_acc;
       CG_HIP(cg::launch_resident_backward(g, N, a, s));
     } else {
-      const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
-      float* ring = reinterpret_cast<float*>(rest);
-      float* dA = reinterpret_cast<float*>(rest + w.ring);
+      float* dA = reinterpret_cast<float*>(rest);
       const int NM = N * M;
       // dBasis = dy W^T written k-major ([K][N*M][Fin]), then the reverse
-      // recurrence one launch per step in the sample-major layout
+      // recurrence one launch per step in the sample-major layout.  Step k
+      // reads D_k[r] and writes G_k[r] at the same address (same lane), and
+      // the steps below k gather G_{k+1} / read G_{k+2} from planes k+1 / k+2,
+      // so G lives in place of dBasis: no separate ring (for config D at
+      // N = 256 that is 3 x 17.2 GB less workspace).
       const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
       if (cg::rowgemm_ok(Fout, Fout, Fin))  // plane k: dA_k[r][fin] = sum_f dy[r][f] W[fin*K+k][f]
         CG_HIP(cg::launch_rowgemm(dy, NM, Fout, Fout, W, 1, int64_t(K) * Fout, Fout, K, Fin, dA, Fin,
@@ -716,25 +710,21 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       else
         CG_HIP(cg::launch_gemm_f32(false, true, NM, FinK, Fout, dy, Fout, W, Fout, dA, FinK, 1, s, K));
       const int* rperm = (Fin >= 16) ? plan->trperm : nullptr;
-      auto G = [&](int k) { return ring + size_t(k % 3) * slot; };
+      auto G = [&](int k) { return dA + size_t(k) * slot; };
       for (int k = K - 1; k >= 0; --k)
         CG_HIP(cg::launch_clenshaw(plan->trowptr, plan->tcol, plan->tval, rperm,
                                    (k + 1 <= K - 1) ? G(k + 1) : nullptr,
                                    (k + 2 <= K - 1) ? G(k + 2) : nullptr, k == 0 ? dx : G(k),
-                                   dA + size_t(k) * slot, N, M, Fin, K, k, dx_acc, s));
+                                   G(k), N, M, Fin, K, k, dx_acc, s));
     }
   }
   if (!dW) return ok();
-  if (!fused && !(cg::g_debug_flags & (1 << 22)))  // ablation hook: skip dW
-    CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, sdw));
-  if (overlap) {
-    CG_HIP(hipEventRecord(plan->ev_join, plan->side));
-    CG_HIP(hipStreamWaitEvent(s, plan->ev_join, 0));
-  }
+  if (!fused && !(cg::debug_flags() & (1 << 22)))  // ablation hook (debug build): skip dW
+    CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, s));
   if (adam)  // reduction + optimizer step in one launch (no exchange in between)
     CG_HIP(cg::launch_reduce_slabs_adam(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, *adam,
                                         s));
-  else if (!(cg::g_debug_flags & (1 << 23)))  // ablation hook: skip the slab reduction
+  else if (!(cg::debug_flags() & (1 << 23)))  // ablation hook (debug build): skip the reduction
     CG_HIP(cg::launch_reduce_slabs(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, s));
   return ok();
 }
@@ -770,6 +760,15 @@ int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int3
                           void* stream) {
   if (!dW || !W || !m || !v || step < 1)
     return fail(CG_ERR_ARG, "cheb_backward_adam: dW, W, m, v required and step >= 1");
+  // the reduction stores grad[i] and then updates param/m/v[i] in place:
+  // any two of them sharing memory would corrupt the update
+  const void* bufs[4] = {dW, W, m, v};
+  for (int i = 0; i < 4; ++i)
+    for (int j = i + 1; j < 4; ++j)
+      if (bufs[i] == bufs[j])
+        return fail(CG_ERR_ARG, "cheb_backward_adam: dW, W, m and v must be distinct buffers");
+  if (cg::debug_flags() & ((1 << 22) | (1 << 23)))
+    return fail(CG_ERR_UNSUPPORTED, "cheb_backward_adam: dW ablation bits would corrupt W");
   cg::AdamStep a{};
   a.param = W;
   a.m = m;

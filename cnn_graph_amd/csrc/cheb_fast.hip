@@ -185,7 +185,7 @@ struct Fwd {
     s_W = reinterpret_cast<float*>(smem + off);
     off = align16(off + size_t(FinK) * Fout * 4);
     s_B = reinterpret_cast<float*>(smem + off);
-    keep_basis = a.basis != nullptr && !(a.dbg & 2);
+    keep_basis = a.basis != nullptr && !CG_DBG(a.dbg, 2);
   }
 
   // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA; stage the basis.
@@ -211,7 +211,7 @@ struct Fwd {
             a = lds_f(ring + mb[t] + soff + fin * 4);
             if (keep_basis && m < M) s_B[m * FinK + fin * K + kk] = a;
           }
-          if (!(A.dbg & 4)) {
+          if (!CG_DBG(A.dbg, 4)) {
 #pragma unroll
             for (int q = 0; q < NT; ++q) acc[t][q] = mfma32(a, b[q], acc[t][q]);
           }
@@ -225,7 +225,7 @@ struct Fwd {
 #pragma clang fp contract(off)
     const V a = r.template dot<FV, L, PRV>(ring);
     V o;
-    if (A.dbg & 32) {  // A/B switch: T_{k-2} of the own row re-read from the ring
+    if (CG_DBG(A.dbg, 32)) {  // A/B switch: T_{k-2} of the own row re-read from the ring
       const V p = lds_v<FV>(ring + r.rr + PRV2 * 4 * FV);
       o = (k == 1) ? a : rec2(a, p);
     } else {           // T_{k-2} of the own row kept in registers (this thread wrote it)
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) c.acc[t][q][e] = 0.f;
   __syncthreads();
-  if (A.dbg & 16) return;
+  if (CG_DBG(A.dbg, 16)) return;
 
   switch (wl) {
 #define CG_L(L_) case L_: c.template run<L_>(); break;
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
     }
   }
 
-  if (A.y && !(A.dbg & 8)) {
+  if (A.y && !CG_DBG(A.dbg, 8)) {
     float* yn = A.y + size_t(n) * M * Fout;
 #pragma unroll
     for (int t = 0; t < F::MT; ++t) {
@@ -417,7 +417,7 @@ struct Bwd {
     if (i >= 1) a = r.template dot<FV, L, NX1>(ring);
     // G_{k+2} of the own row: kept in registers (this thread wrote it two
     // steps ago); debug bit 32 re-reads it from the ring (A/B switch)
-    const V p = (A.dbg & 32) ? lds_v<FV>(ring + r.rr + NX2 * 4 * FV) : g2;
+    const V p = CG_DBG(A.dbg, 32) ? lds_v<FV>(ring + r.rr + NX2 * 4 * FV) : g2;
     const int rr = r.row < 0 ? 0 : r.row;
     V g;
 #pragma unroll
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
   for (int i = tid; i < 32 * 3 * FV; i += kT)  // the 32 zero records
     reinterpret_cast<float*>(smem + A.E.zpos * REC)[i] = 0.f;
   __syncthreads();
-  if (A.dbg & 16) return;
+  if (CG_DBG(A.dbg, 16)) return;
 
   // A. dBasis = dy W^T  (rows m, cols j = fin*K + k, inner f) on MFMA into LDS
   auto store_D = [&](const f32x16& acc, int mt, int j) {
@@ -496,7 +496,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
       }
     }
   };
-  if (!(A.dbg & 2)) {
+  if (!CG_DBG(A.dbg, 2)) {
     if (fastA) {
       const int j = li;
       const bool jv = j < FinK;

@@ -119,6 +119,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
   constexpr int MT = 2 * RPT;  // 32-vertex tiles per wave: ceil(M/32)/16 <= 2*RPT
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M = A.M, K = A.K, Fout = A.Fout, Mp = A.Mp, dbg = A.dbg;
+  (void)dbg;  // only read by the debug build's ablation switches
   const int Fin = FIN1 ? 1 : A.Fin;
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
   for (int i = tid; i < 3 * Fin; i += kT)  // zero words gathered by padding entries
     lds_st(s_T + (i / 3) * slab + M * 12 + (i % 3) * 4, 0.f);
   __syncthreads();
-  if (dbg & 16) return;
+  if (CG_DBG(dbg, 16)) return;
 
   const int ntiles = (M + 31) >> 5;
   f32x16 acc[MT][NT];
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
     for (int q = 0; q < NT; ++q)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][q][r] = 0.f;
-  const bool keep_basis = A.basis && !(dbg & 2);
+  const bool keep_basis = A.basis && !CG_DBG(dbg, 2);
 
   // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA; stage the basis.
   auto mfma_pair = [&](int s) {
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
             a = lds_f(Tb + m * 12);
             if (keep_basis) s_B[m * FinK + fin * K + kk] = a;  // banks (FinK*li+kk) mod 32
           }
-          if (!(dbg & 4)) {
+          if (!CG_DBG(dbg, 4)) {
 #pragma unroll
             for (int q = 0; q < NT; ++q) acc[t][q] = mfma32(a, b[q], acc[t][q]);
           }
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
       for (int q = 0; q < RPT; ++q) {
         if (rows.row[q] >= 0) {
           char* rp = Tb + rows.rb[q];
-          const float a = (dbg & 1) ? lds_f(rp + PRV * 4)
+          const float a = CG_DBG(dbg, 1) ? lds_f(rp + PRV * 4)
                                     : rows.template dot<PRV>(q, Tb, A.col, A.val);
           const float o = (k == 1) ? a : (2.f * a - lds_f(rp + PRV2 * 4));
           lds_st(rp + CUR * 4, o);
@@ -234,7 +235,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_resident(ResidentFwdArgs A) {
     }
   }
 
-  if (A.y && !(dbg & 8)) {
+  if (A.y && !CG_DBG(dbg, 8)) {
     float* yn = A.y + size_t(n) * M * Fout;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
@@ -267,6 +268,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(ResidentBwdArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M = A.M, K = A.K, Fout = A.Fout, Mp = A.Mp, dbg = A.dbg;
+  (void)dbg;
   const int Fin = FIN1 ? 1 : A.Fin;
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(ResidentBwdArgs A) {
   for (int i = tid; i < 3 * Fin; i += kT)
     lds_st(s_G + (i / 3) * slab + M * 12 + (i % 3) * 4, 0.f);
   __syncthreads();
-  if (dbg & 16) return;
+  if (CG_DBG(dbg, 16)) return;
 
   // A. dBasis = dy W^T  (rows m, cols j = fin*K + k, inner f) on MFMA into LDS
   auto store_D = [&](const f32x16& acc, int mt, int j) {
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(ResidentBwdArgs A) {
       }
     }
   };
-  if (!(dbg & 1)) {
+  if (!CG_DBG(dbg, 1)) {
     if (RPT == 1 && fastA) {
       const int j = li;
       const bool jv = j < FinK;
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_resident(ResidentBwdArgs A) {
         const int r = rows.row[q];
         if (r >= 0) {
           char* rp = Gb + rows.rb[q];
-          const float a = (i >= 1) ? ((dbg & 2) ? lds_f(rp + NX1 * 4)
+          const float a = (i >= 1) ? (CG_DBG(dbg, 2) ? lds_f(rp + NX1 * 4)
                                                 : rows.template dot<NX1>(q, Gb, A.col, A.val))
                                    : 0.f;
           float g = Dk[r] + c * a;

@@ -111,6 +111,9 @@ __device__ __forceinline__ void adam_elem(float* __restrict__ param, float* __re
                                           float* __restrict__ v, int64_t i, float grad,
                                           float grad_scale, float lr_t, float beta1, float beta2,
                                           float eps) {
+#pragma clang fp contract(off)
+  // one rounding per operation (no FMA contraction), as TF's ApplyAdam CPU
+  // functor evaluates it; k_adam and k_reduce_slabs_adam therefore agree bitwise
   const float g = grad * grad_scale;
   const float mi = m[i] + (g - m[i]) * (1.f - beta1);
   const float vi = v[i] + (g * g - v[i]) * (1.f - beta2);

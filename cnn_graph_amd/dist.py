@@ -71,6 +71,48 @@ def shard(n_global: int, rank: int, world: int):
     return lo, hi
 
 
+def share_unique_id(uid: bytes, group=None, device=None) -> bytes:
+    """Rank 0's 128-byte communicator id, broadcast to every rank of ``group``
+    (the out-of-band step RCCL leaves to the caller).  nccl groups broadcast
+    a device tensor, gloo groups a host tensor."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return bytes(uid)
+    t = torch.frombuffer(bytearray(bytes(uid).ljust(128, b"\0")[:128]), dtype=torch.uint8).clone()
+    if dist.get_backend(group) == "nccl":
+        t = t.cuda(device)
+    dist.broadcast(t, src=0, group=group)
+    return bytes(t.cpu().tolist())
+
+
+class TorchComm:
+    """The gradient exchange of a training step (``allreduce_sum_`` + ``world``,
+    the interface ResGNN / bench use) over a torch.distributed process group:
+    a ProcessGroupNCCL (RCCL) all_reduce on the device tensor, or -- for gloo
+    groups, e.g. ranks that share one GPU in a test -- through a host copy."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.backend = dist.get_backend(group) if dist.is_initialized() else None
+
+    def allreduce_sum_(self, t: torch.Tensor, stream=None):
+        """In-place SUM over ranks (enqueued after the work on t's current
+        stream; ``stream`` is accepted for interface parity and must be that stream)."""
+        if self.world == 1:
+            return t
+        if self.backend == "nccl" or not t.is_cuda:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            host = t.detach().cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=self.group)
+            t.copy_(host)
+        return t
+
+    def close(self):
+        pass
+
+
 class RcclComm:
     """An RCCL communicator of libcheb_mi355 (cg_comm_* in the C ABI) over the
     ranks of a torch.distributed group: rank 0 creates the unique id, the group
@@ -87,11 +129,7 @@ class RcclComm:
         if self.rank == 0:
             _lib.call("cg_comm_unique_id", uid)
         if self.world > 1:
-            t = torch.frombuffer(bytearray(uid.raw), dtype=torch.uint8).clone()
-            if dist.get_backend(group) == "nccl":
-                t = t.cuda(device)
-            dist.broadcast(t, src=0, group=group)
-            uid = ctypes.create_string_buffer(bytes(t.cpu().tolist()), 128)
+            uid = ctypes.create_string_buffer(share_unique_id(uid.raw, group, device), 128)
         h = ctypes.c_void_p()
         _lib.call("cg_comm_init", ctypes.byref(h), self.world, self.rank, uid, int(device))
         self._h = h

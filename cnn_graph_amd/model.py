@@ -84,8 +84,9 @@ class ResGNN:
         self.step_count = 0
         fb = max(self.plan.workspace_bytes(N, fi, K, fo)[0] for _, fi, fo, _ in layers)
         bb = max(self.plan.workspace_bytes(N, fi, K, fo)[1] for _, fi, fo, _ in layers)
-        self.fws = torch.empty(max(fb, 1), device=self.device, dtype=torch.uint8)
-        self.bws = torch.empty(max(bb, 1), device=self.device, dtype=torch.uint8)
+        # one workspace serves every forward and backward call (stream order:
+        # a call's workspace is dead once the call has executed)
+        self.fws = self.bws = torch.empty(max(fb, bb, 1), device=self.device, dtype=torch.uint8)
         self.fws_n, self.bws_n = fb, bb
         nb = ctypes.c_size_t()
         _lib.call("cg_mse_loss_workspace_bytes", N * M * Fout_last, ctypes.byref(nb))

@@ -29,7 +29,7 @@ def _f32p(a):
 class ChebPlan:
     """Owns a ``cg_plan`` (device CSR of L~ and L~^T)."""
 
-    def __init__(self, Lt, device: int = 0, path: str = "auto"):
+    def __init__(self, Lt, device: int = 0, path: str = "auto", variant: str = "auto"):
         rowptr, col, val = _graph.canonical_csr(Lt)
         self.M = int(Lt.shape[0])
         self.nnz = int(len(col))
@@ -40,12 +40,14 @@ class ChebPlan:
                   _i32p(rowptr), _i32p(col), _f32p(val), None, None, None)
         self._h = h
         self._lib = _lib.lib()
+        self._ws = {}
+        self.set_variant(variant)
         self.set_path(path)
 
     @classmethod
-    def from_laplacian(cls, L, lmax=2, device: int = 0, path: str = "auto"):
+    def from_laplacian(cls, L, lmax=2, device: int = 0, path: str = "auto", variant: str = "auto"):
         """L~ = rescale_L(L, lmax) then a plan (lib/graph_conv.py:148-149)."""
-        return cls(_graph.rescale_L(L, lmax), device=device, path=path)
+        return cls(_graph.rescale_L(L, lmax), device=device, path=path, variant=variant)
 
     @property
     def handle(self):
@@ -55,6 +57,25 @@ class ChebPlan:
         _lib.call("cg_plan_set_path", self._h, _lib.PATHS[path])
         self.path = path
         self._shape_cache = {}
+
+    def set_variant(self, variant: str):
+        """Kernel variant ('auto', 'classic', 'unfused_dw'): same results, other kernels."""
+        _lib.call("cg_plan_set_variant", self._h, _lib.VARIANTS[variant])
+        self.variant = variant
+        self._shape_cache = {}
+
+    def workspace(self, nbytes: int, device, stream_id: int):
+        """A device workspace of at least ``nbytes`` owned by the plan and reused
+        by every call enqueued on the same stream (stream order makes the reuse
+        safe: a call's workspace is dead once the call has executed).  Grown,
+        never shrunk; one buffer per (device, stream)."""
+        import torch
+        key = (str(device), int(stream_id))
+        buf = self._ws.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), device=device, dtype=torch.uint8)
+            self._ws[key] = buf
+        return buf
 
     def _shape_info(self, N, Fin, K, Fout):
         key = (int(N), int(Fin), int(K), int(Fout))
@@ -78,6 +99,7 @@ class ChebPlan:
         return self._shape_info(N, Fin, K, Fout)[1:]
 
     def close(self):
+        self._ws = {}
         if getattr(self, "_h", None) is not None and self._h.value:
             self._lib.cg_plan_destroy(self._h)
             self._h = ctypes.c_void_p()

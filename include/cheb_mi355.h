@@ -51,6 +51,15 @@ enum {
   CG_PATH_STREAM = 2    /* one launch per Chebyshev step + MFMA GEMMs (any size)    */
 };
 
+/* Kernel variant for cg_plan_set_variant (default CG_VARIANT_AUTO).  Every
+ * variant computes the same result (the basis bit-exactly); they exist for
+ * A/B measurement and as independent cross-checks in the tests. */
+enum {
+  CG_VARIANT_AUTO = 0,       /* fastest kernels that fit (cheb_fast when it applies)  */
+  CG_VARIANT_CLASSIC = 1,    /* classic resident kernels (cheb_resident)              */
+  CG_VARIANT_UNFUSED_DW = 2  /* fast kernels, dW by the separate streaming GEMM       */
+};
+
 typedef struct cg_plan cg_plan;
 typedef struct cg_comm cg_comm;
 
@@ -73,11 +82,15 @@ int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz,
                    const int32_t* t_rowptr, const int32_t* t_col, const float* t_val);
 int cg_plan_destroy(cg_plan* plan);
 int cg_plan_set_path(cg_plan* plan, int path);
+int cg_plan_set_variant(cg_plan* plan, int variant);
 /* Which path cg_cheb_forward/backward would take for this shape (CG_PATH_*). */
 int cg_plan_query_path(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                        int* path);
 
-/* Device workspace the forward / backward need for this shape (bytes; may be 0). */
+/* Device workspace the forward / backward need for this shape (bytes; may be 0).
+ * The forward's workspace is dead once the forward call has been enqueued and
+ * executed, so one buffer of max(fwd, bwd) bytes may serve both calls of a
+ * training step on one stream. */
 int cg_cheb_workspace_bytes(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                             size_t* fwd_bytes, size_t* bwd_bytes);
 

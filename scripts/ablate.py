@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Timing ablations of the resident kernels (outputs are garbage when a flag is
 set -- timing only).  Interleaved rounds in one process (guide §5.4 rule 24).
+Runs on the DEBUG build of the library (`make debug`: the ablation switches
+are compiled out of the release .so), loaded through CG_LIB_PATH.
 
-  python scripts/ablate.py [--batch 256] [--reps 50] [--rounds 5]
+  make debug && python scripts/ablate.py [--batch 256] [--reps 50] [--rounds 5]
 """
 import argparse
 import json
@@ -14,17 +16,19 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("CG_LIB_PATH", os.path.join(ROOT, "scripts", "_debug", "libcheb_mi355_debug.so"))
 import bench  # noqa: E402
 from cnn_graph_amd import _lib, ops  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
-# raw cg_debug_set_flags values: bits 0-7 forward kernel, 8-15 backward kernel,
-# 22 skip dW, 23 skip slab reduce, 24 classic resident kernels, 25 no fused dW
-FWD = {"full": 0, "no_basis_store": 2, "no_mfma": 4, "no_y_store": 8, "no_stores": 2 | 8,
-       "only_spmm": 2 | 4 | 8, "prologue": 16, "classic": 1 << 24, "ring_tkm2": 32}
-BWD = {"full": 0, "no_phaseA": 2 << 8, "prologue": 16 << 8, "no_fused_dw": 1 << 25,
-       "no_dw": (1 << 25) | (1 << 22), "no_reduce": 1 << 23, "classic": 1 << 24,
-       "ring_gkp2": 32 << 8}
+# (cg_debug_set_flags value, plan variant): flag bits 0-7 forward kernel,
+# 8-15 backward kernel, 22 skip dW, 23 skip slab reduce
+FWD = {"full": (0, "auto"), "no_basis_store": (2, "auto"), "no_mfma": (4, "auto"),
+       "no_y_store": (8, "auto"), "no_stores": (2 | 8, "auto"), "only_spmm": (2 | 4 | 8, "auto"),
+       "prologue": (16, "auto"), "classic": (0, "classic"), "ring_tkm2": (32, "auto")}
+BWD = {"full": (0, "auto"), "no_phaseA": (2 << 8, "auto"), "prologue": (16 << 8, "auto"),
+       "no_fused_dw": (0, "unfused_dw"), "no_dw": (1 << 22, "unfused_dw"),
+       "no_reduce": (1 << 23, "auto"), "classic": (0, "classic"), "ring_gkp2": (32 << 8, "auto")}
 
 
 def main():
@@ -42,11 +46,13 @@ def main():
     x = torch.rand((N, M, Fin), device=dev)
     W = torch.randn((K, Fout), device=dev) * 0.1
     dy = torch.randn((N, M, Fout), device=dev)
-    r = ops.ChebRunner(plan, N, Fin, K, Fout, dev)
+    runners = {v: ops.ChebRunner(ChebPlan.from_laplacian(L, 2, 0, path=args.path, variant=v),
+                                 N, Fin, K, Fout, dev) for v in ("auto", "classic", "unfused_dw")}
+    r = runners["auto"]
     h = _lib.lib()
     h.cg_debug_set_flags.argtypes = [ctypes_int()]
 
-    def t_fwd():
+    def t_fwd(r):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(args.reps):
@@ -55,7 +61,7 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / args.reps * 1e3
 
-    def t_bwd():
+    def t_bwd(r):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(args.reps):
@@ -68,12 +74,13 @@ def main():
     res.update({f"bwd:{k}": [] for k in BWD})
     r.forward(x, W)
     for _ in range(args.rounds):
-        for k, f in FWD.items():
+        for k, (f, v) in FWD.items():
             h.cg_debug_set_flags(f)
-            res[f"fwd:{k}"].append(t_fwd())
-        for k, f in BWD.items():
+            res[f"fwd:{k}"].append(t_fwd(runners[v]))
+        for k, (f, v) in BWD.items():
+            runners[v].forward(x, W)
             h.cg_debug_set_flags(f)
-            res[f"bwd:{k}"].append(t_bwd())
+            res[f"bwd:{k}"].append(t_bwd(runners[v]))
     h.cg_debug_set_flags(0)
     out = {k: round(float(np.median(v)), 2) for k, v in res.items()}
     # K sweep: per-step cost = slope of time vs K
@@ -81,8 +88,8 @@ def main():
     for Kx in (2, 7, 13, 25):
         Wx = torch.randn((Kx, Fout), device=dev) * 0.1
         rx = ops.ChebRunner(plan, N, Fin, Kx, Fout, dev)
-        for name, f in (("fwd_full", 0), ("fwd_only_spmm", FWD["only_spmm"]), ("bwd_full", 0),
-                        ("bwd_no_dw", BWD["no_dw"])):
+        for name, f in (("fwd_full", 0), ("fwd_only_spmm", FWD["only_spmm"][0]), ("bwd_full", 0),
+                        ("bwd_no_dw", 1 << 22)):
             vals = []
             for _ in range(args.rounds):
                 if name.startswith("fwd"):

@@ -18,7 +18,19 @@ def test_library_exports_every_header_symbol(built_lib):
 
 
 def test_version(built_lib):
-    assert _lib.lib().cg_version() == 200
+    assert _lib.lib().cg_version() == 201
+
+
+def test_release_library_has_no_ablation_hooks(built_lib):
+    """The timing-ablation switches (outputs WRONG when set) exist only in the
+    debug build (`make debug`); the shipping library must not export them."""
+    h = _lib.lib()
+    assert not hasattr(h, "cg_debug_set_flags")
+
+
+def test_plan_variant_validation(built_lib):
+    h = _lib.lib()
+    assert h.cg_plan_set_variant(None, 0) == _lib.CG_ERR_ARG
 
 
 def _i32(a):
@@ -54,6 +66,12 @@ def test_null_and_shape_errors(built_lib):
     assert h.cg_cheb_backward_adam(None, 1, 1, 2, 1, None, None, None, None, None, None, None,
                                    1e-3, 0.9, 0.999, 1e-8, 1, 1.0, None, 0, None) == _lib.CG_ERR_ARG
     assert "backward_adam" in h.cg_last_error().decode()
+    # aliasing of dW / W / m / v is rejected before any device work
+    p = ctypes.c_void_p(4096)
+    q, r = ctypes.c_void_p(8192), ctypes.c_void_p(12288)
+    assert h.cg_cheb_backward_adam(None, 1, 1, 2, 1, None, None, p, None, p, q, r,
+                                   1e-3, 0.9, 0.999, 1e-8, 1, 1.0, None, 0, None) == _lib.CG_ERR_ARG
+    assert "distinct" in h.cg_last_error().decode()
     with pytest.raises(_lib.CGError):
         _lib.call("cg_plan_set_path", None, 0)
 

@@ -1,7 +1,11 @@
 """World-size-2 data-parallel logic on CPU (gloo): batch sharding + ONE fused
 gradient all-reduce reproduces the full-batch gradient and keeps replicas in
 lock-step.  Per-shard gradients come from the oracle (test infrastructure
-standing in for the device kernels, which need a GPU)."""
+standing in for the device kernels, which need a GPU).  Also the exchange
+objects the training step drives (dist.TorchComm.allreduce_sum_ on a flat
+buffer laid out like ResGNN's, and the RCCL unique-id broadcast of
+dist.RcclComm, share_unique_id) over a real 2-rank gloo group.  The same step
+with the HIP kernels at world size 2 is tests/test_gpu_dp.py."""
 import os
 import socket
 
@@ -43,6 +47,18 @@ def _worker(rank, world, port, q):
         cdist.allreduce_gradients([g1, g2], average=False)
         W = torch.tensor(c["W"]) * (rank + 1)
         cdist.broadcast_parameters([W])
+        # the exchange object of ResGNN.train_step on a flat gradient buffer
+        # whose views are the per-layer gradients (one collective per step)
+        flat = torch.arange(12, dtype=torch.float32) * (rank + 1)
+        views = [flat[:5].view(5, 1), flat[5:].view(7, 1)]
+        comm = cdist.TorchComm()
+        assert comm.world == world and comm.rank == rank
+        comm.allreduce_sum_(flat)
+        assert torch.equal(views[1].flatten(), torch.arange(5, 12, dtype=torch.float32) * 3)
+        # RcclComm's out-of-band unique-id step: rank 0's bytes everywhere
+        uid = bytes([rank * 7 + i % 5 for i in range(128)])
+        got = cdist.share_unique_id(uid)
+        assert got == bytes([i % 5 for i in range(128)]), "unique id not rank 0's"
         q.put((rank, g1.numpy(), g2.numpy(), W.numpy()))
         dist.barrier()
         dist.destroy_process_group()

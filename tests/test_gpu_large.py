@@ -4,11 +4,15 @@
      by importing lib/graph.py): basis bit-exact to lib/graph.py::chebyshev,
      y / dx / dW within 1e-5 of the float64 truth; full layer-1 batch (N=128)
      and a Fin=32 layer-2 shape against the oracle.
+     Plus the two-layer stack at the config's batch: layer 1 (Fin 1 -> 32,
+     ReLU) chained into layer 2 (Fin 32 -> 32), forward and backward.
   D: the seeded Chung-Lu power-law graph (scripts/synth_graphs.py, M = 2^18,
      nnz(L~) = 4 189 524, rows up to 1 131 nnz) with Fin = Fout = 64, K = 3:
      one sample against the oracle (whose SpMM order is pinned to the
-     reference's, tests/test_oracle_golden.py), and batch-size-independent
-     identities at a larger batch (per-sample independence, linearity).
+     reference's, tests/test_oracle_golden.py), batch-size-independent
+     identities at N = 16 (per-sample independence, linearity), and the
+     config's full per-rank workload N = 256 (the 2048 global batch over 8
+     GPUs): sampled samples against the oracle and dW against a float64 GEMM.
 """
 import os
 import sys
@@ -140,3 +144,89 @@ def test_config_d_batch_identities(dev, graph_d):
     torch.cuda.synchronize()
     err = O.normwise_err(y12.cpu().numpy(), (2 * y1 + y2).cpu().numpy().astype(np.float64))
     assert err < 1e-5, err
+
+
+@pytest.mark.timeout(600)
+def test_config_c_two_layers_chained_full_batch(dev, graph_c):
+    """Config C as the two-layer stack it is (BASELINE: "2 cheb layers",
+    SURVEY §8d F = [32, 32]) at its batch N = 128: h = relu(cheb(x; W1)) with
+    Fin 1 -> 32, y = cheb(h; W2) with Fin 32 -> 32, then the backward of both.
+    Each layer is checked against the oracle on the inputs it actually got:
+    layer 2's basis bit-exact on the GPU's h, every output / gradient within
+    1e-5 of float64 (the ReLU mask of the backward is the GPU's h > 0)."""
+    from cnn_graph_amd import ops
+    rp, ci, v, M = graph_c["Lt_rowptr"], graph_c["Lt_col"], graph_c["Lt_val"], graph_c["M"]
+    N, K, F1, F2 = 128, 5, 32, 32
+    rng = np.random.default_rng(2048)
+    x = rng.random((N, M, 1), dtype=np.float32)
+    W1 = (rng.standard_normal((1 * K, F1)) * 0.1).astype(np.float32)
+    W2 = (rng.standard_normal((F1 * K, F2)) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((N, M, F2)).astype(np.float32)
+    plan = plan_of(rp, ci, v, M)
+    assert plan.query_path(N, F1, K, F2) == "stream"
+    b1, h = ops.cheb_forward(plan, t(x, dev), t(W1, dev), K, act="relu")
+    b2, y = ops.cheb_forward(plan, h, t(W2, dev), K)
+    dh, dW2 = ops.cheb_backward(plan, t(dy, dev), b2, t(W2, dev), K)
+    dx, dW1, _ = ops.cheb_backward_ex(plan, dh, h, "relu", b1, t(W1, dev), K)
+    torch.cuda.synchronize()
+    hg = h.cpu().numpy()
+    # layer 1
+    ob1, oy1 = O.cheb_forward(x, rp, ci, v, W1, K)
+    assert np.array_equal(b1.cpu().numpy(), ob1)
+    assert O.normwise_err(hg, np.maximum(oy1, 0)) < TOL
+    # layer 2 on the GPU's h
+    ob2, oy2 = O.cheb_forward(hg, rp, ci, v, W2, K)
+    assert np.array_equal(b2.cpu().numpy(), ob2), "layer-2 basis not bit-exact"
+    assert O.normwise_err(y.cpu().numpy(), oy2) < TOL
+    odh, odW2 = O.cheb_backward(dy, ob2, W2, rp, ci, v, N, M, F1, K)
+    assert O.normwise_err(dh.cpu().numpy(), odh) < TOL
+    assert O.normwise_err(dW2.cpu().numpy(), odW2) < TOL
+    dz = np.where(hg > 0, dh.cpu().numpy().astype(np.float64), 0.0)
+    odx, odW1 = O.cheb_backward(dz, ob1, W1, rp, ci, v, N, M, 1, K)
+    assert O.normwise_err(dx.cpu().numpy(), odx) < TOL
+    assert O.normwise_err(dW1.cpu().numpy(), odW1) < TOL
+
+
+@pytest.mark.timeout(900)
+def test_config_d_full_per_rank_batch(dev, graph_d):
+    """Config D at its per-rank workload: N = 256 (2 048 over 8 GPUs),
+    M = 2^18, Fin = Fout = 64, K = 3 -- x, dy, y, dx 17.2 GB each, the basis
+    51.5 GB and one shared 51.5 GB workspace (ChebRunner; the reverse
+    recurrence runs in place of dBasis), ~172 GB of the 288 GB HBM.  Samples
+    0, 131 and 255: basis bit-exact, y and dx within 1e-5 of the float64
+    oracle; dW (a sum over all 256 samples) within 1e-5 of a float64 GEMM of
+    the same basis and dy."""
+    from cnn_graph_amd import ops
+    rp, ci, v, M = graph_d
+    N, Fin, K, Fout = 256, 64, 3, 64
+    FinK = Fin * K
+    plan = plan_of(rp, ci, v, M)
+    assert plan.query_path(N, Fin, K, Fout) == "stream"
+    fb, bb = plan.workspace_bytes(N, Fin, K, Fout)
+    assert max(fb, bb) <= 4 * N * M * FinK + (64 << 20)
+    run = ops.ChebRunner(plan, N, Fin, K, Fout, dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2017)
+    x = torch.rand((N, M, Fin), device=dev, generator=g)
+    W = torch.randn((FinK, Fout), device=dev, generator=g) * 0.1
+    dy = torch.randn((N, M, Fout), device=dev, generator=g)
+    y = run.forward(x, W)
+    dx, dW = run.backward(dy, W)
+    torch.cuda.synchronize()
+    Wn = W.cpu().numpy()
+    basis = run.basis.view(N, M, FinK)
+    for n in (0, 131, 255):
+        xn = x[n:n + 1].cpu().numpy()
+        dyn = dy[n:n + 1].cpu().numpy()
+        ob, oy = O.cheb_forward(xn, rp, ci, v, Wn, K)
+        assert np.array_equal(basis[n].cpu().numpy(), ob), f"sample {n}: basis not bit-exact"
+        assert O.normwise_err(y[n:n + 1].cpu().numpy(), oy) < TOL
+        odx, _ = O.cheb_backward(dyn, ob, Wn, rp, ci, v, 1, M, Fin, K)
+        assert O.normwise_err(dx[n:n + 1].cpu().numpy(), odx) < TOL
+    ref = torch.zeros((FinK, Fout), dtype=torch.float64, device=dev)
+    for c in range(0, N, 16):
+        bc = run.basis[c * M:(c + 16) * M].double()
+        ref += bc.t() @ dy[c:c + 16].reshape(-1, Fout).double()
+        del bc
+    torch.cuda.synchronize()
+    assert O.normwise_err(dW.cpu().numpy(), ref.cpu().numpy()) < TOL

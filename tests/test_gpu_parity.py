@@ -26,28 +26,22 @@ def dev(built_lib):
     return torch.device("cuda", 0)
 
 
-# Kernel variants of the resident path (debug bits of cg_debug_set_flags):
+# Kernel variants of the resident path (cg_plan_set_variant, per plan):
 # "fast" = cheb_fast.hip with the fused dW (default), "fast_nofuse" = fast
 # kernels + the separate dW GEMM, "classic" = cheb_resident.hip.
-VARIANTS = {"fast": 0, "fast_nofuse": 1 << 25, "classic": 1 << 24}
+VARIANTS = {"fast": "auto", "fast_nofuse": "unfused_dw", "classic": "classic"}
 
 
 @pytest.fixture(params=list(VARIANTS))
 def variant(request, dev):
-    import ctypes
-    from cnn_graph_amd import _lib
-    h = _lib.lib()
-    h.cg_debug_set_flags.argtypes = [ctypes.c_int]
-    h.cg_debug_set_flags(VARIANTS[request.param])
-    yield request.param
-    h.cg_debug_set_flags(0)
+    return VARIANTS[request.param]
 
 
-def make_plan(c, path):
+def make_plan(c, path, variant="auto"):
     from cnn_graph_amd.plan import ChebPlan
     M = c["M"]
     Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
-    return ChebPlan(Lt, device=0, path=path)
+    return ChebPlan(Lt, device=0, path=path, variant=variant)
 
 
 def t(a, dev):
@@ -63,7 +57,7 @@ def test_native_library_is_the_in_tree_build(dev):
 
 @pytest.mark.parametrize("fname,prefix", CASES, ids=CASE_IDS)
 def test_resident_variants_golden(dev, variant, fname, prefix):
-    test_forward_backward_golden(dev, fname, prefix, "resident")
+    test_forward_backward_golden(dev, fname, prefix, "resident", variant)
 
 
 @pytest.mark.parametrize("fin", [1, 2, 4])
@@ -77,7 +71,7 @@ def test_fast_path_fin_widths_vs_oracle(dev, variant, fin):
     x = rng.random((N, c["M"], fin), dtype=np.float32)
     W = (rng.standard_normal((fin * K, Fout)) * 0.1).astype(np.float32)
     dy = rng.standard_normal((N, c["M"], Fout)).astype(np.float32)
-    plan = make_plan(c, "resident")
+    plan = make_plan(c, "resident", variant)
     basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), K)
     dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), K)
     torch.cuda.synchronize()
@@ -91,10 +85,10 @@ def test_fast_path_fin_widths_vs_oracle(dev, variant, fin):
 
 @pytest.mark.parametrize("path", ["resident", "stream"])
 @pytest.mark.parametrize("fname,prefix", CASES, ids=CASE_IDS)
-def test_forward_backward_golden(dev, fname, prefix, path):
+def test_forward_backward_golden(dev, fname, prefix, path, variant="auto"):
     from cnn_graph_amd import ops
     c = case(load_golden(fname), prefix)
-    plan = make_plan(c, path)
+    plan = make_plan(c, path, variant)
     assert plan.query_path(c["N"], c["Fin"], c["K"], c["Fout"]) == path
     x, W, dy = t(c["x"], dev), t(c["W"], dev), t(c["dy"], dev)
     basis, y = ops.cheb_forward(plan, x, W, c["K"])
@@ -119,18 +113,11 @@ def test_config_b_full_batch_vs_oracle(dev, path):
     x[:, g["fake_rows"], :] = 0
     W = c["W"]
     dy = rng.standard_normal((N, c["M"], c["Fout"])).astype(np.float32)
-    import ctypes
-    from cnn_graph_amd import _lib
-    h = _lib.lib()
-    h.cg_debug_set_flags.argtypes = [ctypes.c_int]
-    h.cg_debug_set_flags(VARIANTS["classic"] if path == "classic" else 0)
-    try:
-        plan = make_plan(c, "resident" if path == "classic" else path)
-        basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), c["K"])
-        dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), c["K"])
-        torch.cuda.synchronize()
-    finally:
-        h.cg_debug_set_flags(0)
+    plan = make_plan(c, "resident" if path == "classic" else path,
+                     "classic" if path == "classic" else "auto")
+    basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), c["K"])
+    dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), c["K"])
+    torch.cuda.synchronize()
     ob, oy = O.cheb_forward(x, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], W, c["K"])
     assert np.array_equal(basis.cpu().numpy(), ob)
     assert O.normwise_err(y.cpu().numpy(), oy) < TOL
