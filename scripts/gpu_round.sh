@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { echo SMOKE_FAIL; tail -30 $OUT/smoke.txt; exit 1; }
 tail -1 $OUT/smoke.txt
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest_gpu.txt; exit 1; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest_gpu.txt; exit 1; }
 tail -1 $OUT/pytest_gpu.txt
 timeout -k 10 240 python scripts/ablate.py > $OUT/ablate.json 2>&1 || { echo ABLATE_FAIL; tail -20 $OUT/ablate.json; exit 1; }
 grep -v amdgpu.ids $OUT/ablate.json | head -30
