@@ -9,7 +9,11 @@ SRCS     := $(SRC_DIR)/cheb_fast.hip $(SRC_DIR)/cheb_resident.hip $(SRC_DIR)/che
             $(SRC_DIR)/lstm.hip $(SRC_DIR)/epilogue.hip $(SRC_DIR)/fourier.hip \
             $(SRC_DIR)/cheb_abi.cpp $(SRC_DIR)/comm.cpp $(SRC_DIR)/coarsen.cpp \
             $(SRC_DIR)/lds_layout.cpp
-OBJS     := $(patsubst $(SRC_DIR)/%,$(OBJ_DIR)/%.o,$(SRCS))
+# fast resident kernels: one object per instantiation of cheb_fast_kern.h
+# (fastf_<Fin>_<Fout tiles>, fastb_<Fin>_<fused dW>), compiled in parallel
+FAST_INST := fastf_1_1 fastf_1_2 fastf_2_1 fastf_2_2 fastf_4_1 fastf_4_2 \
+             fastb_1_0 fastb_1_1 fastb_2_0 fastb_2_1 fastb_4_0 fastb_4_1
+OBJS     := $(patsubst $(SRC_DIR)/%,$(OBJ_DIR)/%.o,$(SRCS)) $(patsubst %,$(OBJ_DIR)/%.o,$(FAST_INST))
 DEPS     := $(OBJS:.o=.d)
 
 all: $(LIB)
@@ -20,11 +24,23 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%
 	@mkdir -p $(OBJ_DIR)
 	$(HIPCC) $(CXXFLAGS) -MMD -MP -c $< -o $@
 
+w1 = $(word 1,$(subst _, ,$*))
+w2 = $(word 2,$(subst _, ,$*))
+$(OBJ_DIR)/fastf_%.o: $(SRC_DIR)/cheb_fast_inst.hip
+	@mkdir -p $(OBJ_DIR)
+	$(HIPCC) $(CXXFLAGS) -DCG_FAST_FWD -DCG_FV=$(w1) -DCG_NT=$(w2) -MMD -MP -c $< -o $@
+$(OBJ_DIR)/fastb_%.o: $(SRC_DIR)/cheb_fast_inst.hip
+	@mkdir -p $(OBJ_DIR)
+	$(HIPCC) $(CXXFLAGS) -DCG_FAST_BWD -DCG_FV=$(w1) -DCG_DW=$(w2) -MMD -MP -c $< -o $@
+
 $(LIB): $(OBJS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 -include $(DEPS)
+# dependency files are never remade (else make's built-in `%: %.o` link rule
+# would try to build fastf_1_1.d from fastf_1_1.d.o through the pattern below)
+$(DEPS): ;
 
 # Ablation build (scripts/ablate.py, via CG_LIB_PATH): the same sources with
 # -DCG_DEBUG, which compiles in cg_debug_set_flags and the kernels' timing

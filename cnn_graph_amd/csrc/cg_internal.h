@@ -30,7 +30,11 @@ __host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(
 extern int g_debug_flags;
 #define CG_DBG(flags, bit) (((flags) & (bit)) != 0)
 inline int debug_flags() { return g_debug_flags; }
+// tuning overrides of the ablation build (cg_debug_set_param); -1 = default
+extern int g_debug_params[8];
+inline int debug_param(int i, int dflt) { return g_debug_params[i] >= 0 ? g_debug_params[i] : dflt; }
 #else
+constexpr int debug_param(int, int dflt) { return dflt; }
 #define CG_DBG(flags, bit) false
 constexpr int debug_flags() { return 0; }
 #endif

@@ -18,6 +18,7 @@
 #ifdef CG_DEBUG
 namespace cg {
 int g_debug_flags = 0;
+int g_debug_params[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
 }
 #endif
 
@@ -369,6 +370,13 @@ int cg_version(void) { return 201; }
 // public header, not in the release library; outputs are WRONG when set).
 int cg_debug_set_flags(int flags) {
   cg::g_debug_flags = flags;
+  return ok();
+}
+// Tuning override (ablation build only): launch code reads key k < 8 with
+// cg::debug_param(k, default); value -1 restores the default.
+int cg_debug_set_param(int key, int value) {
+  if (key < 0 || key >= 8) return fail(CG_ERR_ARG, "bad debug param %d", key);
+  cg::g_debug_params[key] = value;
   return ok();
 }
 #endif
