@@ -57,6 +57,10 @@ _SIGNATURES = {
                              _c_i32, _vp, _vp, _vp, _c_sz, _vp], _c_int),
     "cg_mse_loss_workspace_bytes": ([_c_i64, ctypes.POINTER(_c_sz)], _c_int),
     "cg_mse_loss": ([_vp, _vp, _c_i64, _vp, _vp, _vp, _c_sz, _vp], _c_int),
+    "cg_mse_loss_ema": ([_vp, _vp, _c_i64, _vp, _vp, _vp, ctypes.c_float, _vp, _c_sz, _vp], _c_int),
+    "cg_slice_channels": ([_vp, _c_i64, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
+    "cg_stack_merge_forward": ([_c_i32, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp], _c_int),
+    "cg_stack_merge_backward": ([_c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp], _c_int),
     "cg_weight_grad_workspace_bytes": ([_c_i64, _c_i32, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
     "cg_weight_grad": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
     "cg_bias_grad_workspace_bytes": ([_c_i64, _c_i32, ctypes.POINTER(_c_sz)], _c_int),

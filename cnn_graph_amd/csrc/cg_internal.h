@@ -219,8 +219,17 @@ hipError_t launch_bias_act_bwd(const float* dy, const float* y, int act, int64_t
                                hipStream_t s);
 // loss = mean((labels - pred)^2) (fixed-order reduction); dpred = 2 (pred - labels) / n
 int mse_chunks(int64_t n);
+// ema: optional float[3] {biased, average, local_step} of the loss moving
+// average (ExponentialMovingAverage(decay), zero-debiased), updated in place
 hipError_t launch_mse(const float* pred, const float* labels, int64_t n, float* slab, float* loss,
-                      float* dpred, hipStream_t s);
+                      float* dpred, hipStream_t s, float* ema = nullptr, float decay = 0.9f);
+// stacked-input ResGNN pieces (lib/graph_conv.py:272-303)
+hipError_t launch_slice_channels(const float* x, int64_t rows, int C, int c0, int c1, float* out,
+                                 hipStream_t s);
+hipError_t launch_stack_merge_fwd(const float* o, const float* w, int N, int64_t MF, int accumulate,
+                                  float* y, hipStream_t s);
+hipError_t launch_stack_merge_bwd(const float* dy, const float* o, const float* w, int N, int64_t MF,
+                                  float* d_o, float* dw, hipStream_t s);
 
 // ---- gconv-LSTM cell (lstm.hip) ------------------------------------------------
 // gates: 0 = reference gate functions (tan / sigmoid / sigmoid / tanh,

@@ -829,6 +829,47 @@ int cg_mse_loss(const float* pred, const float* labels, int64_t n, float* loss, 
   return ok();
 }
 
+int cg_mse_loss_ema(const float* pred, const float* labels, int64_t n, float* loss, float* dpred,
+                    float* ema, float decay, void* workspace, size_t ws_bytes, void* stream) {
+  if (!pred || !labels || !loss || !ema || n < 1 || !(decay >= 0.f && decay <= 1.f))
+    return fail(CG_ERR_ARG, "mse_loss_ema: bad arguments");
+  const size_t need = al256(size_t(cg::mse_chunks(n)) * 4);
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "mse_loss_ema workspace too small: %zu < %zu", ws_bytes, need);
+  CG_HIP(cg::launch_mse(pred, labels, n, static_cast<float*>(workspace), loss, dpred,
+                        reinterpret_cast<hipStream_t>(stream), ema, decay));
+  return ok();
+}
+
+int cg_slice_channels(const float* x, int64_t rows, int32_t C, int32_t c0, int32_t c1, float* out,
+                      void* stream) {
+  if (!x || !out || rows < 1 || C < 1 || c0 < 0 || c1 <= c0 || c1 > C)
+    return fail(CG_ERR_ARG, "slice_channels: bad arguments (C=%d, [%d, %d))", C, c0, c1);
+  CG_HIP(cg::launch_slice_channels(x, rows, C, c0, c1, out, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_stack_merge_forward(int32_t N, int32_t M, int32_t F, const float* out_i, const float* w_i,
+                           int32_t accumulate, float* y, void* stream) {
+  if (N < 1 || M < 1 || F < 1 || !out_i || !w_i || !y)
+    return fail(CG_ERR_ARG, "stack_merge_forward: bad arguments");
+  if (out_i == y) return fail(CG_ERR_ARG, "stack_merge_forward: y must not alias out_i");
+  CG_HIP(cg::launch_stack_merge_fwd(out_i, w_i, N, int64_t(M) * F, accumulate, y,
+                                    reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_stack_merge_backward(int32_t N, int32_t M, int32_t F, const float* dy, const float* out_i,
+                            const float* w_i, float* dout_i, float* dw_i, void* stream) {
+  if (N < 1 || M < 1 || F < 1 || !dy || !out_i || !w_i || (!dout_i && !dw_i))
+    return fail(CG_ERR_ARG, "stack_merge_backward: bad arguments");
+  if (dout_i && (dout_i == out_i || dout_i == dy))
+    return fail(CG_ERR_ARG, "stack_merge_backward: dout_i must not alias dy / out_i");
+  CG_HIP(cg::launch_stack_merge_bwd(dy, out_i, w_i, N, int64_t(M) * F, dout_i, dw_i,
+                                    reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
 int cg_weight_grad_workspace_bytes(int64_t R, int32_t FinK, int32_t Fout, size_t* bytes) {
   if (!bytes || R < 1 || FinK < 1 || Fout < 1) return fail(CG_ERR_ARG, "weight_grad: bad arguments");
   *bytes = dw_slab_bytes(R, 0, FinK, Fout);

@@ -8,7 +8,12 @@
 //               and-filter (b2relu, :195-199) bias; dz = dy * act'(y)
 //   k_mse_*     loss = mean((labels - pred)^2), dpred = 2 (pred - labels) / n
 //               (tf.reduce_mean(tf.square(tf.subtract(labels, logits))),
-//               lib/graph_model.py:255), fixed-order two-stage reduction.
+//               lib/graph_model.py:255), fixed-order two-stage reduction, plus
+//               the loss moving average of :265-273 (optional)
+//   k_slice_channels / k_stack_merge_*
+//               the stacked-input ResGNN (_inference with stack_num > 1,
+//               lib/graph_conv.py:272-303): channel groups of the input, and
+//               X = sum_i relu(net_i(x_i)) * w_i with w_i [M][F] broadcast over N
 // The fast resident forward and the streaming row GEMM apply the residual /
 // ReLU epilogue in their own y store; these kernels are the fallback.
 #include "cg_internal.h"
@@ -93,8 +98,14 @@ __global__ __launch_bounds__(256) void k_mse_part(const float* __restrict__ pred
   if (threadIdx.x == 0) slab[blockIdx.x] = part[0];
 }
 
+// ema (optional, float[3] = {biased, average, local_step}): TF-1.x
+// ExponentialMovingAverage(decay).apply([loss]) of a Tensor, i.e.
+// assign_moving_average(zero_debias=True) (moving_averages.py):
+//   d1 = 1 - decay; biased -= (biased - loss) * d1; step += 1;
+//   average -= average - biased / (1 - (1 - d1)^step)
 __global__ __launch_bounds__(256) void k_mse_final(const float* __restrict__ slab, int nslab,
-                                                   float inv_n, float* __restrict__ loss) {
+                                                   float inv_n, float* __restrict__ loss,
+                                                   float* __restrict__ ema, float decay) {
 #pragma clang fp contract(off)
   __shared__ float part[256];
   float s = 0.f;
@@ -105,7 +116,71 @@ __global__ __launch_bounds__(256) void k_mse_final(const float* __restrict__ sla
     if (int(threadIdx.x) < w) part[threadIdx.x] = part[threadIdx.x] + part[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) *loss = part[0] * inv_n;
+  if (threadIdx.x == 0) {
+    const float l = part[0] * inv_n;
+    *loss = l;
+    if (ema) {
+      const float d1 = 1.f - decay;
+      const float biased = ema[0] - (ema[0] - l) * d1;
+      const float step = ema[2] + 1.f;
+      const float bias_factor = 1.f - powf(1.f - d1, step);
+      ema[0] = biased;
+      ema[1] = ema[1] - (ema[1] - biased / bias_factor);
+      ema[2] = step;
+    }
+  }
+}
+
+// out[r][c] = x[r][c0 + c], c < w: the channel group x[..., c0:c0+w] of an
+// [rows][C] tensor (the reshape / unstack / concat of lib/graph_conv.py:281-286)
+__global__ __launch_bounds__(256) void k_slice_channels(const float* __restrict__ x, int64_t rows,
+                                                        int C, int c0, int w,
+                                                        float* __restrict__ out) {
+  const int64_t n = rows * w;
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    const int64_t r = i / w;
+    out[i] = x[r * C + c0 + (i - r * w)];
+  }
+}
+
+// y = (accumulate ? y : 0) + relu(o) * w[i mod MF]   (lib/graph_conv.py:297-301:
+// X = x1 * w1, then X = X + x1 * w1 with x1 = relu(residual_network(x_i)))
+__global__ __launch_bounds__(256) void k_stack_merge_fwd(const float* __restrict__ o,
+                                                         const float* __restrict__ w, int64_t n,
+                                                         int64_t MF, int accumulate,
+                                                         float* __restrict__ y) {
+#pragma clang fp contract(off)
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    const float x1 = o[i] > 0.f ? o[i] : 0.f;
+    const float v = x1 * w[i % MF];
+    y[i] = accumulate ? y[i] + v : v;
+  }
+}
+
+// TF gradients of X (+)= relu(o) * w: dx1 = dy * w (Mul grad, no reduction on
+// x1's side), do = ReluGrad(dx1, relu(o)) = o > 0 ? dx1 : 0
+__global__ __launch_bounds__(256) void k_stack_merge_bwd(const float* __restrict__ dy,
+                                                         const float* __restrict__ o,
+                                                         const float* __restrict__ w, int64_t n,
+                                                         int64_t MF, float* __restrict__ d_o) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+    d_o[i] = o[i] > 0.f ? dy[i] * w[i % MF] : 0.f;
+}
+
+// dw[j] = sum_n relu(o[n][j]) * dy[n][j], n ascending (the broadcast reduction of
+// the Mul gradient over the batch axis; fixed order, bitwise reproducible)
+__global__ __launch_bounds__(256) void k_stack_merge_dw(const float* __restrict__ dy,
+                                                        const float* __restrict__ o, int N,
+                                                        int64_t MF, float* __restrict__ dw) {
+#pragma clang fp contract(off)
+  const int64_t j = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= MF) return;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float x1 = o[n * MF + j] > 0.f ? o[n * MF + j] : 0.f;
+    s = s + x1 * dy[n * MF + j];
+  }
+  dw[j] = s;
 }
 
 }  // namespace
@@ -139,13 +214,39 @@ int mse_chunks(int64_t n) {
 }
 
 hipError_t launch_mse(const float* pred, const float* labels, int64_t n, float* slab, float* loss,
-                      float* dpred, hipStream_t s) {
+                      float* dpred, hipStream_t s, float* ema, float decay) {
   const int chunks = mse_chunks(n);
   const int64_t chunk = (n + chunks - 1) / chunks;
   hipLaunchKernelGGL(k_mse_part, dim3(chunks), dim3(256), 0, s, pred, labels, n, chunk,
                      float(2.0 / double(n)), slab, dpred);
   hipLaunchKernelGGL(k_mse_final, dim3(1), dim3(256), 0, s, slab, chunks, float(1.0 / double(n)),
-                     loss);
+                     loss, ema, decay);
+  return hipGetLastError();
+}
+
+hipError_t launch_slice_channels(const float* x, int64_t rows, int C, int c0, int c1, float* out,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(k_slice_channels, dim3(grid1d(rows * (c1 - c0), 256)), dim3(256), 0, s, x, rows,
+                     C, c0, c1 - c0, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_stack_merge_fwd(const float* o, const float* w, int N, int64_t MF, int accumulate,
+                                  float* y, hipStream_t s) {
+  const int64_t n = int64_t(N) * MF;
+  hipLaunchKernelGGL(k_stack_merge_fwd, dim3(grid1d(n, 256)), dim3(256), 0, s, o, w, n, MF,
+                     accumulate, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_stack_merge_bwd(const float* dy, const float* o, const float* w, int N, int64_t MF,
+                                  float* d_o, float* dw, hipStream_t s) {
+  const int64_t n = int64_t(N) * MF;
+  if (d_o)
+    hipLaunchKernelGGL(k_stack_merge_bwd, dim3(grid1d(n, 256)), dim3(256), 0, s, dy, o, w, n, MF, d_o);
+  if (dw)
+    hipLaunchKernelGGL(k_stack_merge_dw, dim3(int((MF + 255) / 256)), dim3(256), 0, s, dy, o, N, MF,
+                       dw);
   return hipGetLastError();
 }
 

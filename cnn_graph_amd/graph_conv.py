@@ -191,6 +191,29 @@ class GraphConv:
             x = self.filter(x, L, Fout_last, K)
         return x
 
+    def inference(self, x, L, nfilter, K, nres_layer_count, stack_num=1, groups=((0, 12), (12, 16)),
+                  Fout_last=2):
+        """``_inference`` (lib/graph_conv.py:272-303).  stack_num == 1: the
+        residual network on x.  stack_num > 1: channel group i of x (the
+        reference hard-codes [0:12] and [12:16], :284-285) through its own
+        residual network in scope final_merge/VC_i, ReLU, merged as
+        X = sum_i relu(net_i) * w_i with w_i = final_merge/W_i/weights [M, Fout_last]."""
+        if stack_num == 1:
+            return self.residual_network(x, L, nfilter, K, nres_layer_count, Fout_last)
+        if len(groups) != stack_num:
+            raise ValueError(f"stack_num={stack_num} needs {stack_num} channel groups, got {len(groups)}")
+        C = int(x.shape[-1])
+        X = None
+        with self.variable_scope("final_merge"):
+            for i, (a, b) in enumerate(groups):
+                xi = x if (a, b) == (0, C) else ops.slice_channels(x, a, b)
+                with self.variable_scope(f"VC_{i}"):
+                    x1 = self.residual_network(xi, L, nfilter, K, nres_layer_count, Fout_last)
+                with self.variable_scope(f"W_{i}"):
+                    w1 = self._weight_variable([int(x1.shape[1]), int(x1.shape[2])])
+                X = ops.stack_merge(x1, w1, X)
+        return X
+
     # -- the pooled multi-level cgcnn (lib/models.py:61-127, usage.ipynb) ------------
     @staticmethod
     def select_laplacians(L, p):

@@ -580,3 +580,65 @@ def fourier_conv(x, W, U):
     """filter_in_fourier (lib/graph_conv.py:83-99): x [N, M, Fin], W [M, Fout,
     Fin], U [M, M] (eigenvectors in columns, device fp32) -> [N, M, Fout]."""
     return _Fourier.apply(x, W, U)
+
+
+# -- stacked-input ResGNN pieces (lib/graph_conv.py:272-303) -----------------------
+class _SliceChannels(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, c0: int, c1: int):
+        _check_dev("x", x)
+        x = x.contiguous()
+        C = int(x.shape[-1])
+        rows = x.numel() // C
+        out = torch.empty(tuple(x.shape[:-1]) + (c1 - c0,), device=x.device, dtype=torch.float32)
+        _lib.call("cg_slice_channels", _p(x), rows, C, int(c0), int(c1), _p(out), _stream(x))
+        ctx.shape, ctx.c0, ctx.c1 = tuple(x.shape), c0, c1
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        raise RuntimeError("slice_channels: the input channels are data (no gradient), "
+                           "as in lib/graph_conv.py:274-303")
+
+
+def slice_channels(x, c0: int, c1: int):
+    """x[..., c0:c1] of a [N, M, C] device tensor as a new contiguous tensor
+    (the reshape / unstack / concat of lib/graph_conv.py:281-286)."""
+    return _SliceChannels.apply(x, int(c0), int(c1))
+
+
+class _StackMerge(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out_i, w_i, acc):
+        for name, t in (("out_i", out_i), ("w_i", w_i)):
+            _check_dev(name, t)
+        out_i, w_i = out_i.contiguous(), w_i.contiguous()
+        N, M, F = (int(s) for s in out_i.shape)
+        if tuple(w_i.shape) != (M, F):
+            raise ValueError(f"merge weight must be [{M}, {F}], got {tuple(w_i.shape)}")
+        y = torch.empty_like(out_i)
+        if acc is not None:
+            y.copy_(acc)  # (buffer plumbing: the kernel accumulates into y)
+        _lib.call("cg_stack_merge_forward", N, M, F, _p(out_i), _p(w_i), int(acc is not None), _p(y),
+                  _stream(out_i))
+        ctx.save_for_backward(out_i, w_i)
+        ctx.has_acc = acc is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        out_i, w_i = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, M, F = (int(s) for s in out_i.shape)
+        d_o = torch.empty_like(out_i) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(w_i) if ctx.needs_input_grad[1] else None
+        if d_o is not None or dw is not None:
+            _lib.call("cg_stack_merge_backward", N, M, F, _p(dy), _p(out_i), _p(w_i), _p(d_o), _p(dw),
+                      _stream(dy))
+        return d_o, dw, (dy if ctx.has_acc else None)
+
+
+def stack_merge(out_i, w_i, acc=None):
+    """acc + relu(out_i) * w_i (w_i [M, F] broadcast over N; acc None: no add)
+    -- one term of X = sum_i relu(net_i) * w_i, lib/graph_conv.py:292-301."""
+    return _StackMerge.apply(out_i, w_i, acc)

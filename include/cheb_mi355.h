@@ -145,6 +145,30 @@ int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_
 int cg_mse_loss_workspace_bytes(int64_t n, size_t* bytes);
 int cg_mse_loss(const float* pred, const float* labels, int64_t n, float* loss, float* dpred,
                 void* workspace, size_t ws_bytes, void* stream);
+/* The same, and the loss moving average of lib/graph_model.py:265-273
+ * (tf.train.ExponentialMovingAverage(decay).apply([loss]), zero-debiased as TF
+ * does for a Tensor): ema = device float[3] {biased, average, local_step},
+ * zero-initialised by the caller, updated in place; average is loss_average. */
+int cg_mse_loss_ema(const float* pred, const float* labels, int64_t n, float* loss, float* dpred,
+                    float* ema, float decay, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Stacked-input ResGNN, GraphConv._inference with stack_num > 1
+ * (lib/graph_conv.py:272-303): the input's channel groups feed separate
+ * residual networks whose outputs merge as X = sum_i relu(net_i) * w_i,
+ * w_i [M][F] (tf.get_variable 'final_merge/W_i/weights') broadcast over N.
+ *   cg_slice_channels:  out [rows][c1-c0] = x[rows][C][c0:c1]
+ *   cg_stack_merge_forward:  y = (accumulate ? y : 0) + relu(out_i) * w_i
+ *   cg_stack_merge_backward: dout_i = out_i > 0 ? dy * w_i : 0 and
+ *       dw_i[m][f] = sum_n relu(out_i[n][m][f]) dy[n][m][f] (n ascending);
+ *       either output may be NULL.
+ * ------------------------------------------------------------------------- */
+int cg_slice_channels(const float* x, int64_t rows, int32_t C, int32_t c0, int32_t c1, float* out,
+                      void* stream);
+int cg_stack_merge_forward(int32_t N, int32_t M, int32_t F, const float* out_i, const float* w_i,
+                           int32_t accumulate, float* y, void* stream);
+int cg_stack_merge_backward(int32_t N, int32_t M, int32_t F, const float* dy, const float* out_i,
+                            const float* w_i, float* dout_i, float* dw_i, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Weight gradient of the contraction on its own (the tf.matmul gradient of

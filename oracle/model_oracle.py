@@ -84,3 +84,64 @@ def train_step(x, labels, Ws, lap, K, R, adam_state, step, lr):
         new_W.append(W2)
         new_state.append((m2, v2))
     return loss, dWs, new_W, new_state
+
+
+# ---- stacked-input ResGNN: _inference with stack_num > 1 (lib/graph_conv.py:272-303)
+def stacked_forward(x, nets, merge_Ws, groups, lap, K, R):
+    """x [N, M, C]; nets[i] = Ws of network i (forward()'s layout), merge_Ws[i]
+    [M, F].  X = sum_i relu(net_i(x[..., a_i:b_i])) * w_i (:284-301).
+    Returns (X, caches)."""
+    X = None
+    caches = []
+    for (a, b), Ws, w in zip(groups, nets, merge_Ws):
+        out, cache = forward(np.asarray(x, np.float64)[..., a:b], Ws, lap, K, R)
+        x1 = np.maximum(out, 0)                                   # (:292)
+        X = x1 * w if X is None else X + x1 * w                   # (:297-301)
+        caches.append((out, cache))
+    return X, caches
+
+
+def stacked_backward(dX, caches, nets, merge_Ws, lap, K, R):
+    """Returns (dWs per network, dw per merge weight)."""
+    dnets, dws = [], []
+    for (out, cache), Ws, w in zip(caches, nets, merge_Ws):
+        x1 = np.maximum(out, 0)
+        dws.append(np.sum(dX * x1, axis=0))                       # Mul grad, reduced over N
+        dout = dX * w * (out > 0)                                  # Mul grad, then ReluGrad
+        dnets.append(backward(dout, cache, Ws, lap, K, R))
+    return dnets, dws
+
+
+def ema_update(state, value, decay=0.9):
+    """tf.train.ExponentialMovingAverage(decay).apply([loss]) of a Tensor
+    (lib/graph_model.py:265-273): zero-debiased assign_moving_average.
+    state = (biased, average, local_step); returns the new state."""
+    biased, avg, step = state
+    d1 = 1.0 - decay
+    biased = biased - (biased - value) * d1
+    step = step + 1
+    avg = avg - (avg - biased / (1.0 - (1.0 - d1) ** step))
+    return biased, avg, step
+
+
+def stacked_train_step(x, labels, nets, merge_Ws, groups, lap, K, R, adam_state, step, lr):
+    """One step; adam_state in the order net_0 weights, w_0, net_1 weights, w_1, ...
+    Returns (loss, grads in that order, new nets, new merge_Ws, new adam_state)."""
+    X, caches = stacked_forward(x, nets, merge_Ws, groups, lap, K, R)
+    loss, dX = loss_and_grad(X, labels)
+    dnets, dws = stacked_backward(dX, caches, nets, merge_Ws, lap, K, R)
+    flat_W, flat_g = [], []
+    for Ws, w, gs, gw in zip(nets, merge_Ws, dnets, dws):
+        flat_W += list(Ws) + [w]
+        flat_g += list(gs) + [gw]
+    new_flat, new_state = [], []
+    for W, g, (m, v) in zip(flat_W, flat_g, adam_state):
+        W2, m2, v2 = O.adam_step(W, g, m, v, step, lr=lr)
+        new_flat.append(W2)
+        new_state.append((m2, v2))
+    new_nets, new_merge, i = [], [], 0
+    for Ws in nets:
+        new_nets.append(new_flat[i:i + len(Ws)])
+        new_merge.append(new_flat[i + len(Ws)])
+        i += len(Ws) + 1
+    return loss, flat_g, new_nets, new_merge, new_state

@@ -92,3 +92,19 @@ def test_lstm_and_grad_entry_points_validate(built_lib):
     assert h.cg_lstm_cell_backward(4, 2, 0, None, None, None, None, None, None, None, None, None) == _lib.CG_ERR_ARG
     assert h.cg_lstm_cell_forward(1 << 30, 8, 0, 1, None, None, None, 1, 1, None, None) == _lib.CG_ERR_ARG
     assert "2^31" in h.cg_last_error().decode()
+
+
+def test_stack_merge_and_loss_ema_entry_points_validate(built_lib):
+    """stack_num > 1 pieces and the loss moving average reject bad arguments
+    before any device work (no GPU needed)."""
+    h = _lib.lib()
+    p, q, r = ctypes.c_void_p(4096), ctypes.c_void_p(8192), ctypes.c_void_p(12288)
+    assert h.cg_slice_channels(p, 10, 16, 12, 17, q, None) == _lib.CG_ERR_ARG
+    assert "[12, 17)" in h.cg_last_error().decode()
+    assert h.cg_slice_channels(p, 10, 16, 4, 4, q, None) == _lib.CG_ERR_ARG
+    assert h.cg_stack_merge_forward(2, 10, 2, p, q, 0, p, None) == _lib.CG_ERR_ARG
+    assert "alias" in h.cg_last_error().decode()
+    assert h.cg_stack_merge_backward(2, 10, 2, p, q, r, None, None, None) == _lib.CG_ERR_ARG
+    assert h.cg_stack_merge_backward(2, 10, 2, p, q, r, p, None, None) == _lib.CG_ERR_ARG
+    assert h.cg_mse_loss_ema(p, q, 10, r, None, None, 0.9, None, 0, None) == _lib.CG_ERR_ARG
+    assert h.cg_mse_loss_ema(p, q, 10, r, None, r, 1.5, None, 0, None) == _lib.CG_ERR_ARG

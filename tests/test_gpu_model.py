@@ -137,3 +137,82 @@ def test_graphconv_residual_network_autograd_matches_trainer(dev):
     torch.cuda.synchronize()
     for name, g in model.gradients().items():
         assert O.normwise_err(f64(gc.weights[name].grad), f64(g)) < 1e-5, name
+
+
+@pytest.mark.parametrize("graph,R,F", [("golden_E.npz", 1, 8), ("golden_B.npz", 2, 16)])
+def test_stacked_resgnn_train_steps_vs_oracle(dev, graph, R, F):
+    """_inference with stack_num = 2 (lib/graph_conv.py:272-303; the humanflow
+    driver's 16 channels split [0:12] / [12:16]): three optimizer steps vs the
+    float64 oracle -- loss, the loss moving average, every gradient (both
+    networks and both [M, 2] merge weights) and every updated weight."""
+    from cnn_graph_amd.model import StackedResGNN
+    L, _ = golden_L(graph)
+    N, K, C = 3, 4, 16
+    model = StackedResGNN(L, N=N, C=C, nfilter=F, K=K, nres_layer_count=R, learning_rate=1e-2,
+                          decay_rate=0.95, decay_steps=2, device=dev, seed=7)
+    lap = (model.plan.rowptr, model.plan.col, model.plan.val.astype(np.float64))
+    rng = np.random.default_rng(11)
+    x = rng.random((N, model.M, C)).astype(np.float32)
+    labels = rng.random((N, model.M, 2)).astype(np.float32)
+    nl = len(model.nets[0].W)
+    nets = [[f64(w) for w in net.W] for net in model.nets]
+    merge = [f64(w) for w in model.merge_W]
+    state = [(np.zeros_like(w), np.zeros_like(w)) for w in (nets[0] + [merge[0]] + nets[1] + [merge[1]])]
+    ema = (0.0, 0.0, 0)
+    assert len(model.names) == 2 * (nl + 1) and model.names[nl] == "final_merge/W_0/weights"
+    for step in range(1, 4):
+        loss = model.train_step(t(x, dev), t(labels, dev))
+        torch.cuda.synchronize()
+        lr = model.learning_rate(step - 1)
+        rl, rg, nets, merge, state = MO.stacked_train_step(
+            x.astype(np.float64), labels, nets, merge, model.groups, lap, K, R, state, step, lr)
+        ema = MO.ema_update(ema, rl)
+        assert abs(float(loss.item()) - rl) <= 1e-5 * rl, (step, float(loss.item()), rl)
+        assert abs(float(model.loss_average.item()) - ema[1]) <= 1e-5 * ema[1], step
+        for name, g, r in zip(model.names, model.dW, rg):
+            assert O.normwise_err(f64(g), r) < TOL, (step, name)
+        flat_ref = nets[0] + [merge[0]] + nets[1] + [merge[1]]
+        for name, w, r in zip(model.names, model.W, flat_ref):
+            assert O.normwise_err(f64(w), r) < TOL, (step, name)
+
+
+def test_resgnn_loss_average(dev):
+    """ResGNN.train_step keeps the reference's loss moving average
+    (lib/graph_model.py:265-273) on device."""
+    from cnn_graph_amd.model import ResGNN
+    L, _ = golden_L("golden_A.npz")
+    model = ResGNN(L, N=2, Fin=1, nfilter=4, K=3, nres_layer_count=1, device=dev, seed=3)
+    rng = np.random.default_rng(4)
+    x = t(rng.random((2, model.M, 1)), dev)
+    labels = t(rng.random((2, model.M, 2)), dev)
+    ema = (0.0, 0.0, 0)
+    for _ in range(4):
+        loss = model.train_step(x, labels)
+        torch.cuda.synchronize()
+        ema = MO.ema_update(ema, float(loss.item()))
+        assert abs(float(model.loss_average.item()) - ema[1]) <= 1e-6 * ema[1]
+
+
+def test_graphconv_inference_stacked_autograd_matches_trainer(dev):
+    """GraphConv.inference(stack_num=2) (torch autograd over the HIP ops) gives
+    the trainer's loss gradients for every variable, scope names included."""
+    from cnn_graph_amd.graph_conv import GraphConv
+    from cnn_graph_amd.model import StackedResGNN
+    L, _ = golden_L("golden_E.npz")
+    N, K, F, R, C = 2, 3, 8, 1, 16
+    model = StackedResGNN(L, N=N, C=C, nfilter=F, K=K, nres_layer_count=R, device=dev, seed=1)
+    gc = GraphConv(device=dev)
+    rng = np.random.default_rng(5)
+    x = t(rng.random((N, model.M, C)), dev)
+    labels = t(rng.random((N, model.M, 2)), dev)
+    gc.inference(x, L, F, K, R, stack_num=2)
+    assert set(gc.weights) == set(model.names)
+    for name, w in model.parameters().items():
+        with torch.no_grad():
+            gc.weights[name].copy_(w)
+    X = gc.inference(x, L, F, K, R, stack_num=2)
+    ((X - labels) ** 2).mean().backward()
+    model.train_step(x, labels)
+    torch.cuda.synchronize()
+    for name, g in model.gradients().items():
+        assert O.normwise_err(f64(gc.weights[name].grad), f64(g)) < 1e-5, name
