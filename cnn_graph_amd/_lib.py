@@ -18,9 +18,9 @@ CG_OK, CG_ERR_ARG, CG_ERR_HIP, CG_ERR_UNSUPPORTED, CG_ERR_ALLOC, CG_ERR_COMM = r
 CG_PATH_AUTO, CG_PATH_RESIDENT, CG_PATH_STREAM = 0, 1, 2
 CG_ACT_NONE, CG_ACT_RELU, CG_ACT_TANH = 0, 1, 2
 PATHS = {"auto": CG_PATH_AUTO, "resident": CG_PATH_RESIDENT, "stream": CG_PATH_STREAM}
-CG_VARIANT_AUTO, CG_VARIANT_CLASSIC, CG_VARIANT_UNFUSED_DW = 0, 1, 2
+CG_VARIANT_AUTO, CG_VARIANT_CLASSIC, CG_VARIANT_UNFUSED_DW, CG_VARIANT_NARROW = 0, 1, 2, 3
 VARIANTS = {"auto": CG_VARIANT_AUTO, "classic": CG_VARIANT_CLASSIC,
-            "unfused_dw": CG_VARIANT_UNFUSED_DW}
+            "unfused_dw": CG_VARIANT_UNFUSED_DW, "narrow": CG_VARIANT_NARROW}
 
 
 class CGError(RuntimeError):

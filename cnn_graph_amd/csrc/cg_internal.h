@@ -176,6 +176,42 @@ hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val,
 hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tval, const int* rperm,
                            const float* Gn1, const float* Gn2, float* Gout, const float* Dk, int N,
                            int M, int Fin, int K, int k, int dx_acc, hipStream_t s);
+// ---- wide-column streaming path (cheb_wide.hip): Fin < 8, vertex-major [M][Fin*N]
+struct WideGeom {
+  int G;    // column groups (8: one per XCD under round-robin placement, or 1)
+  int CB;   // columns per group
+  int pl;   // floats per lane (1, 2, 4)
+  int rpb;  // rows per 256-thread block
+  bool ok;
+};
+WideGeom wide_geometry(int N, int Fin, int M);
+// mode 0: out = L~ Tp; 1: out = 2 L~ Tp - Tpp; 2: out = Dk + c L~ Tp [- Tpp]
+// (Tp NULL: the sum is +0).  Planes are [M][B], B = Fin*N.
+hipError_t launch_wide_step(const WideGeom& g, const int* rowptr, const int* col, const float* val,
+                            const int* rperm, const float* Tp, const float* Tpp, const float* Dk,
+                            float* out, int M, int B, int mode, float c, hipStream_t s);
+// The last forward step fused with the basis assembly (Fin == 1, natural row
+// order): planes T_0..T_{K-2} in, basis [N][M][K] out.
+bool wide_last_ok(const WideGeom& g, int Fin, int K, bool rperm);
+hipError_t launch_wide_last(const WideGeom& g, const int* rowptr, const int* col, const float* val,
+                            const float* planes, int64_t plane, float* basis, int M, int N, int K,
+                            hipStream_t s);
+// dst[p][q][n] = src[p][n][q] (P planes; Q = M*Fin) and the reverse, dst[n][q] (+)= src[q][n]
+hipError_t launch_sm_to_vm(const float* src, int P, int N, int64_t Q, float* dst, hipStream_t s);
+hipError_t launch_vm_to_sm(const float* src, int N, int64_t Q, float* dst, int accumulate,
+                           hipStream_t s);
+// Backward dense pass of the wide path, one read of dy: D planes
+// D[k*plane + m*Fin*N + fin*N + n] = sum_f dy[n][m][f] W[fin*K+k][f] and per-block
+// dW partials slab[b][FinK][Fout] (wide_dypass_blocks of them; reduce after).
+bool wide_dypass_ok(int FinK, int Fout);
+int wide_dypass_blocks(int N, int M);
+hipError_t launch_wide_dypass(const float* dy, const float* basis, const float* W, int N, int M,
+                              int Fin, int K, int Fout, float* D, int64_t plane, float* slab,
+                              hipStream_t s);
+// basis[n][m][fin*K + k] = T[k*plane + m*Fin*N + fin*N + n]
+hipError_t launch_wide_assemble(const float* T, int64_t plane, int N, int M, int Fin, int K,
+                                float* basis, hipStream_t s);
+
 // C[Mg x Ng] (+)= op(A)[Mg x Kg] * op(B)[Kg x Ng]; fp32 in/out on MFMA f32.
 // trans_a: A stored [Kg][lda] (A^T row-major); trans_b: B stored [Ng][ldb].
 // splits > 1: the K range is cut into `splits` slices, slice s writes
@@ -185,9 +221,13 @@ hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tva
 // r < R, k < Kc, j < Nc.  rowgemm_ok says whether the shape is supported.
 bool rowgemm_ok(int Kc, int lda, int Nc);
 // Epilogue (planes == 1 use): C = act(C + res), res [R][ldc] or NULL, act 1 = ReLU.
+// pfin > 0 (planes == 1, no epilogue): one pass over A computes Nc = P*pfin
+// columns, column jj being column jj % pfin of plane jj / pfin (B and C alike),
+// so A is read once for all planes instead of once per plane.
 hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
                           int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
-                          int64_t c_plane, hipStream_t s, const float* res = nullptr, int act = 0);
+                          int64_t c_plane, hipStream_t s, const float* res = nullptr, int act = 0,
+                          int pfin = 0);
 // remapK > 0: write C in the k-major [remapK][Mg][Ng/remapK] layout instead
 // (column fin*K + k -> plane k), splits must be 1.
 hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, const float* A,

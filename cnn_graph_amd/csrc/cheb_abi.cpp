@@ -320,25 +320,41 @@ int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool bac
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
 struct StreamWs {
-  size_t slots;  // forward: T_1 .. T_{K-2}, (K-2) * N*M*Fin floats
+  bool wide;     // wide-column layout (cheb_wide.hip) for small Fin
+  size_t slots;  // forward: T_1 .. T_{K-2} (sample-major), or the K planes T_0 .. T_{K-1} ([M][B], wide)
   size_t dA;     // backward: dBasis, N*M*FinK floats (k-major); G_k overwrites plane k
+                 // (wide: + the same again for the [K][M][B] planes D_k / G_k)
 };
+
+// The wide-column path serves the streaming path when Fin < 8 (sample-major
+// gathers of Fin*4 < 32 bytes) and its column split fits (cheb_wide.hip).
+bool use_wide(const cg_plan* p, int32_t N, int32_t Fin, int32_t K) {
+  return p->variant != CG_VARIANT_NARROW && int64_t(Fin) * K <= 256 &&
+         cg::wide_geometry(N, Fin, p->M).ok;
+}
 
 StreamWs stream_ws(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t Fout) {
   StreamWs w{};
   const int64_t B = int64_t(N) * Fin;
   const int64_t FinK = int64_t(Fin) * K;
   const int64_t NM = int64_t(N) * p->M;
-  w.slots = al256(size_t(K > 2 ? K - 2 : 0) * size_t(p->M) * size_t(B) * 4);
+  w.wide = use_wide(p, N, Fin, K);
+  const size_t plane = size_t(p->M) * size_t(B) * 4;
+  w.slots = al256(w.wide ? size_t(K) * plane : size_t(K > 2 ? K - 2 : 0) * plane);
   w.dA = al256(size_t(NM) * size_t(FinK) * 4);
+  // wide: the [K][M][B] planes D_k / G_k (+ the sample-major dBasis when the
+  // fused dy pass does not apply)
+  if (w.wide) w.dA = al256(size_t(K) * plane) + (cg::wide_dypass_ok(int(FinK), Fout) ? 0 : w.dA);
   (void)Fout;
   return w;
 }
 
 // dW partial slabs: dw_chunks(R) of them from k_dw_slabs, or one per sample
 // from the fused backward.
-size_t dw_slab_bytes(int64_t R, int32_t N, int FinK, int Fout) {
-  const size_t n = std::max<size_t>(size_t(cg::dw_chunks(R)), size_t(N));
+// M > 0: the wide path's fused dy pass writes the slabs (one per block)
+size_t dw_slab_bytes(int64_t R, int32_t N, int FinK, int Fout, int32_t M = 0) {
+  size_t n = std::max<size_t>(size_t(cg::dw_chunks(R)), size_t(N));
+  if (M > 0) n = std::max<size_t>(n, size_t(cg::wide_dypass_blocks(N, M)));
   return al256(n * size_t(FinK) * size_t(Fout) * 4);
 }
 
@@ -353,7 +369,9 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
   if ((rc = choose_path(p, Fin, K, Fout, false, &pf))) return rc;
   if ((rc = choose_path(p, Fin, K, Fout, true, &pb))) return rc;
   const StreamWs w = stream_ws(p, N, Fin, K, Fout);
-  const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, N, Fin * K, Fout);
+  const bool dypass = pb != CG_PATH_RESIDENT && stream_ws(p, N, Fin, K, Fout).wide &&
+                      cg::wide_dypass_ok(Fin * K, Fout);
+  const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, N, Fin * K, Fout, dypass ? p->M : 0);
   *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.slots;
   *bwd = slabs + ((pb == CG_PATH_RESIDENT) ? 0 : w.dA);
   return CG_OK;
@@ -518,7 +536,7 @@ int cg_plan_set_path(cg_plan* plan, int path) {
 int cg_plan_set_variant(cg_plan* plan, int variant) {
   if (!plan) return fail(CG_ERR_ARG, "null plan");
   if (variant != CG_VARIANT_AUTO && variant != CG_VARIANT_CLASSIC &&
-      variant != CG_VARIANT_UNFUSED_DW)
+      variant != CG_VARIANT_UNFUSED_DW && variant != CG_VARIANT_NARROW)
     return fail(CG_ERR_ARG, "bad kernel variant %d", variant);
   plan->variant = variant;
   return ok();
@@ -609,18 +627,38 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
     return fail(CG_ERR_ARG, "forward workspace too small: %zu < %zu", ws_bytes, w.slots);
   float* slots = static_cast<float*>(workspace);
   const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
-  // sample-major steps: T_0 = x, T_j (1 <= j <= K-2) in slots[j-1], the last
-  // step writes the whole basis (lib/graph_conv.py:159-172)
-  const int* rperm = (Fin >= 16) ? plan->rperm : nullptr;
-  auto T = [&](int k) -> const float* { return k == 0 ? x : slots + size_t(k - 1) * slot; };
-  if (K == 1)
+  if (K == 1) {
     CG_HIP(hipMemcpyAsync(basis, x, slot * sizeof(float), hipMemcpyDeviceToDevice, s));
-  for (int k = 1; k < K; ++k) {
-    const bool last = (k == K - 1);
-    CG_HIP(cg::launch_cheb_step(plan->rowptr, plan->col, plan->val, rperm, T(k - 1),
-                                k >= 2 ? T(k - 2) : nullptr,
-                                last ? nullptr : slots + size_t(k - 1) * slot, x, slots, basis, N,
-                                M, Fin, K, k, last, s));
+  } else if (w.wide) {
+    // wide columns: T_0 = x re-laid [M][Fin*N] into plane 0, the K-1 steps
+    // plane to plane, then the basis (lib/graph_conv.py:155-172)
+    const cg::WideGeom g = cg::wide_geometry(N, Fin, M);
+    const int B = N * Fin;
+    const int* rperm = plan->rperm;
+    const bool fused_last = cg::wide_last_ok(g, Fin, K, rperm != nullptr);
+    CG_HIP(cg::launch_sm_to_vm(x, 1, N, int64_t(M) * Fin, slots, s));
+    for (int k = 1; k < (fused_last ? K - 1 : K); ++k)
+      CG_HIP(cg::launch_wide_step(g, plan->rowptr, plan->col, plan->val, rperm,
+                                  slots + size_t(k - 1) * slot,
+                                  k >= 2 ? slots + size_t(k - 2) * slot : nullptr, nullptr,
+                                  slots + size_t(k) * slot, M, B, k == 1 ? 0 : 1, 2.f, s));
+    if (fused_last)  // T_{K-1} and the basis assembly in one launch
+      CG_HIP(cg::launch_wide_last(g, plan->rowptr, plan->col, plan->val, slots, int64_t(slot), basis,
+                                  M, N, K, s));
+    else
+      CG_HIP(cg::launch_wide_assemble(slots, int64_t(slot), N, M, Fin, K, basis, s));
+  } else {
+    // sample-major steps: T_0 = x, T_j (1 <= j <= K-2) in slots[j-1], the last
+    // step writes the whole basis (lib/graph_conv.py:159-172)
+    const int* rperm = (Fin >= 16) ? plan->rperm : nullptr;
+    auto T = [&](int k) -> const float* { return k == 0 ? x : slots + size_t(k - 1) * slot; };
+    for (int k = 1; k < K; ++k) {
+      const bool last = (k == K - 1);
+      CG_HIP(cg::launch_cheb_step(plan->rowptr, plan->col, plan->val, rperm, T(k - 1),
+                                  k >= 2 ? T(k - 2) : nullptr,
+                                  last ? nullptr : slots + size_t(k - 1) * slot, x, slots, basis, N,
+                                  M, Fin, K, k, last, s));
+    }
   }
   if (y) {
     const int FinK = Fin * K;
@@ -662,9 +700,12 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   // the event fork + join costs ~20 us per call, more than the overlap gains.)
   char* base = static_cast<char*>(workspace);
   float* slabs = reinterpret_cast<float*>(base);
-  char* rest = base + dw_slab_bytes(R, N, FinK, Fout);
+  const bool dypass = path != CG_PATH_RESIDENT && stream_ws(plan, N, Fin, K, Fout).wide &&
+                      cg::wide_dypass_ok(FinK, Fout);
+  char* rest = base + dw_slab_bytes(R, N, FinK, Fout, dypass ? M : 0);
   const bool fused =
       dx != nullptr && dW != nullptr && path == CG_PATH_RESIDENT && fused_dw(plan, Fin, K, Fout);
+  int nslab_ready = 0;  // dW slabs a kernel of the dx pass already wrote
   if (dx) {
     if (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, true)) {
       const cg::FastGeom g = fast_geom(plan, Fin, K, Fout);
@@ -702,6 +743,24 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       a.dx = dx;
       a.dx_acc = dx_acc;
       CG_HIP(cg::launch_resident_backward(g, N, a, s));
+    } else if (dypass) {
+      // wide columns: ONE pass over dy writes the D_k planes straight in the
+      // [M][Fin*N] layout and the dW slabs; then G_k in place of D_k, one
+      // launch per step, and G_0 re-laid into dx (dx += when accumulating)
+      const cg::WideGeom g = cg::wide_geometry(N, Fin, M);
+      const int B = N * Fin;
+      const size_t slot = size_t(M) * size_t(B);
+      float* D = reinterpret_cast<float*>(rest);
+      CG_HIP(cg::launch_wide_dypass(dy, basis, W, N, M, Fin, K, Fout, D, int64_t(slot),
+                                    dW ? slabs : nullptr, s));
+      if (dW) nslab_ready = cg::wide_dypass_blocks(N, M);
+      auto G = [&](int k) { return D + size_t(k) * slot; };
+      for (int k = K - 1; k >= 0; --k)
+        CG_HIP(cg::launch_wide_step(g, plan->trowptr, plan->tcol, plan->tval, plan->trperm,
+                                    (k + 1 <= K - 1) ? G(k + 1) : nullptr,
+                                    (k + 2 <= K - 1) ? G(k + 2) : nullptr, G(k), G(k), M, B, 2,
+                                    k >= 1 ? 2.f : 1.f, s));
+      CG_HIP(cg::launch_vm_to_sm(G(0), N, int64_t(M) * Fin, dx, dx_acc, s));
     } else {
       float* dA = reinterpret_cast<float*>(rest);
       const int NM = N * M;
@@ -712,28 +771,51 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       // so G lives in place of dBasis: no separate ring (for config D at
       // N = 256 that is 3 x 17.2 GB less workspace).
       const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
-      if (cg::rowgemm_ok(Fout, Fout, Fin))  // plane k: dA_k[r][fin] = sum_f dy[r][f] W[fin*K+k][f]
+      // plane k: dA_k[r][fin] = sum_f dy[r][f] W[fin*K+k][f]; all K planes in
+      // one pass over dy when the FinK columns fit one row-GEMM block
+      if (cg::rowgemm_ok(Fout, Fout, FinK))
+        CG_HIP(cg::launch_rowgemm(dy, NM, Fout, Fout, W, 1, int64_t(K) * Fout, Fout, 1, FinK, dA, Fin,
+                                  int64_t(slot), s, nullptr, 0, Fin));
+      else if (cg::rowgemm_ok(Fout, Fout, Fin))
         CG_HIP(cg::launch_rowgemm(dy, NM, Fout, Fout, W, 1, int64_t(K) * Fout, Fout, K, Fin, dA, Fin,
                                   int64_t(slot), s));
       else
         CG_HIP(cg::launch_gemm_f32(false, true, NM, FinK, Fout, dy, Fout, W, Fout, dA, FinK, 1, s, K));
-      const int* rperm = (Fin >= 16) ? plan->trperm : nullptr;
-      auto G = [&](int k) { return dA + size_t(k) * slot; };
-      for (int k = K - 1; k >= 0; --k)
-        CG_HIP(cg::launch_clenshaw(plan->trowptr, plan->tcol, plan->tval, rperm,
-                                   (k + 1 <= K - 1) ? G(k + 1) : nullptr,
-                                   (k + 2 <= K - 1) ? G(k + 2) : nullptr, k == 0 ? dx : G(k),
-                                   G(k), N, M, Fin, K, k, dx_acc, s));
+      const StreamWs w = stream_ws(plan, N, Fin, K, Fout);
+      if (w.wide) {
+        // wide columns: the k-planes re-laid [M][Fin*N], then G_k in place of
+        // D_k one launch per step, G_0 re-laid into dx (dx += when accumulating)
+        const cg::WideGeom g = cg::wide_geometry(N, Fin, M);
+        const int B = N * Fin;
+        float* D = reinterpret_cast<float*>(rest + al256(size_t(R) * size_t(FinK) * 4));
+        CG_HIP(cg::launch_sm_to_vm(dA, K, N, int64_t(M) * Fin, D, s));
+        auto G = [&](int k) { return D + size_t(k) * slot; };
+        for (int k = K - 1; k >= 0; --k)
+          CG_HIP(cg::launch_wide_step(g, plan->trowptr, plan->tcol, plan->tval, plan->trperm,
+                                      (k + 1 <= K - 1) ? G(k + 1) : nullptr,
+                                      (k + 2 <= K - 1) ? G(k + 2) : nullptr, G(k), G(k), M, B, 2,
+                                      k >= 1 ? 2.f : 1.f, s));
+        CG_HIP(cg::launch_vm_to_sm(G(0), N, int64_t(M) * Fin, dx, dx_acc, s));
+      } else {
+        const int* rperm = (Fin >= 16) ? plan->trperm : nullptr;
+        auto G = [&](int k) { return dA + size_t(k) * slot; };
+        for (int k = K - 1; k >= 0; --k)
+          CG_HIP(cg::launch_clenshaw(plan->trowptr, plan->tcol, plan->tval, rperm,
+                                     (k + 1 <= K - 1) ? G(k + 1) : nullptr,
+                                     (k + 2 <= K - 1) ? G(k + 2) : nullptr, k == 0 ? dx : G(k),
+                                     G(k), N, M, Fin, K, k, dx_acc, s));
+      }
     }
   }
   if (!dW) return ok();
-  if (!fused && !(cg::debug_flags() & (1 << 22)))  // ablation hook (debug build): skip dW
+  if (fused) nslab_ready = N;
+  if (!nslab_ready && !(cg::debug_flags() & (1 << 22)))  // ablation hook (debug build): skip dW
     CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, s));
+  const int nslab = nslab_ready ? nslab_ready : chunks;
   if (adam)  // reduction + optimizer step in one launch (no exchange in between)
-    CG_HIP(cg::launch_reduce_slabs_adam(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, *adam,
-                                        s));
+    CG_HIP(cg::launch_reduce_slabs_adam(slabs, nslab, int64_t(FinK) * Fout, dW, *adam, s));
   else if (!(cg::debug_flags() & (1 << 23)))  // ablation hook (debug build): skip the reduction
-    CG_HIP(cg::launch_reduce_slabs(slabs, fused ? N : chunks, int64_t(FinK) * Fout, dW, s));
+    CG_HIP(cg::launch_reduce_slabs(slabs, nslab, int64_t(FinK) * Fout, dW, s));
   return ok();
 }
 

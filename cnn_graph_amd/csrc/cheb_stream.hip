@@ -1,16 +1,22 @@
 // Streaming path of the Chebyshev graph convolution for gfx950: any graph
-// size (the dense right-hand side lives in HBM, one launch per Chebyshev step).
+// size (the dense right-hand side lives in HBM, one launch per Chebyshev step),
+// sample-major layout ([N][M][Fin], the layout of x); small Fin (< 8) runs on
+// the wide-column layout of cheb_wide.hip instead.
 //
-//   x_to_cols   : x [N][M][Fin] -> T_0 [M][B] (column b = n*Fin + fin) and basis k=0
-//   spmm_step   : T_k = 2 L~ T_{k-1} - T_{k-2} (T_1 = L~ T_0), one wave per CSR row,
-//                 lanes over dense columns (16 B per lane when B % 4 == 0), with
-//                 the recurrence fused into the epilogue and the basis column
-//                 fin*K + k of lib/graph_conv.py:172 written in the same pass.
-//   clenshaw    : G_k = D_k + c L~^T G_{k+1} - G_{k+2}, D_k gathered from dBasis,
-//                 k = 0 writes dx directly.
-//   gemm_f32    : LDS-tiled v_mfma_f32_32x32x2_f32 GEMM (64x64 tile, 4 waves),
-//                 optional split-K partial slabs; contraction y = basis W,
-//                 dBasis = dy W^T and dW = basis^T dy.
+//   k_cheb_step / k_cheb_last
+//                 T_k = 2 L~ T_{k-1} - T_{k-2} (T_1 = L~ T_0, T_0 IS x), LPR =
+//                 Fin/VEC lanes per (sample, row), sample-per-XCD block mapping
+//                 for slabs <= 2 MB; the last step assembles the basis rows
+//                 [fin][k] of lib/graph_conv.py:172 (staged in LDS)
+//   k_clenshaw_step
+//                 G_k = D_k + c L~^T G_{k+1} - G_{k+2}, D_k a plane of the
+//                 k-major dBasis, G_k written in place of it; k = 0 writes dx
+//   k_rowgemm     persistent skinny MFMA GEMM (32x32x2 f32, small operand in
+//                 LDS): y = basis W (+ residual / ReLU epilogue) and the k-major
+//                 dBasis planes (all planes in one pass over dy)
+//   k_gemm_f32    LDS-tiled MFMA GEMM for the other shapes
+//   k_dw_slabs / k_reduce_slabs
+//                 dW = basis^T dy as per-chunk slabs, fixed-order reduction
 //
 // The SpMM accumulates sequentially in CSR order with fp contraction off, so
 // the basis is bit-identical to the resident path and to lib/graph.py::chebyshev.
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(256) void k_cheb_last(ChebStepArgs a, StepGeom g) {
 struct RowGemmArgs {
   const float* A;
   int64_t R;
-  int Kc, lda, KC2;        // KC2 = half of Kc rounded up to a multiple of 16
+  int Kc, lda, KC2;        // KC2 = half of Kc (rounded up to a multiple of 16 when Kc >= 32)
   const float* B;          // B_p[k][j] = B[p*bs_p + k*bs_k + j*bs_j]
   int64_t bs_k, bs_j, bs_p;
   int Nc;
@@ -262,6 +268,9 @@ struct RowGemmArgs {
   int64_t c_plane;
   const float* res;  // epilogue: C = act(C + res)
   int act;
+  int pfin;          // > 0: ONE pass computes every plane -- column jj is
+                     // (plane jj / pfin, column jj % pfin) of B and of C
+  int vecA;          // A rows are 16-byte aligned (lda % 4 == 0): float4 loads
 };
 
 template <int NT>
@@ -276,7 +285,11 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
     // row kk of the padded operand: half 0 holds k < KC2, half 1 holds KC2 + (kk - KC2)
     const int k = kk;
     float v = 0.f;
-    if (k < a.Kc && j < a.Nc) v = a.B[p * a.bs_p + int64_t(k) * a.bs_k + int64_t(j) * a.bs_j];
+    if (k < a.Kc && j < a.Nc) {
+      const int pp = a.pfin > 0 ? j / a.pfin : p;
+      const int jj = a.pfin > 0 ? j - pp * a.pfin : j;
+      v = a.B[pp * a.bs_p + int64_t(k) * a.bs_k + int64_t(jj) * a.bs_j];
+    }
     Bs[e] = v;
   }
   __syncthreads();
@@ -296,7 +309,8 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
     for (int c0 = 0; c0 < a.KC2; c0 += 16) {
       float av[16];
       const int k0 = kbeg + c0;
-      if (k0 + 16 <= a.Kc && (kbeg + c0 + 16 <= kbeg + a.KC2)) {
+      const int nq = (a.KC2 - c0 < 16) ? a.KC2 - c0 : 16;  // (small Kc: no padded MFMAs)
+      if (a.vecA && nq == 16 && k0 + 16 <= a.Kc) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const float4 v = *reinterpret_cast<const float4*>(arow + k0 + 4 * q);
@@ -307,20 +321,25 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
         }
       } else {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) av[q] = (k0 + q < a.Kc) ? arow[k0 + q] : 0.f;
+        for (int q = 0; q < 16; ++q) av[q] = (q < nq && k0 + q < a.Kc) ? arow[k0 + q] : 0.f;
       }
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const float* brow = Bs + (kbeg + c0 + q) * NP + i;
+        if (q < nq) {
+          const float* brow = Bs + (kbeg + c0 + q) * NP + i;
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], brow[t * 32], acc[t], 0, 0, 0);
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], brow[t * 32], acc[t], 0, 0, 0);
+        }
       }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int col = t * 32 + i;
-      if (col >= a.Nc) continue;
+      const int jcol = t * 32 + i;
+      if (jcol >= a.Nc) continue;
+      const int pp = a.pfin > 0 ? jcol / a.pfin : 0;
+      const int col = a.pfin > 0 ? jcol - pp * a.pfin : jcol;
+      float* Cp = C + pp * a.c_plane;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -328,7 +347,7 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
           float v = acc[t][q];
           if (a.res) v = v + a.res[rr * a.ldc + col];
           if (a.act) v = v > 0.f ? v : 0.f;
-          C[rr * a.ldc + col] = v;
+          Cp[rr * a.ldc + col] = v;
         }
       }
     }
@@ -579,18 +598,24 @@ hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tva
   return hipGetLastError();
 }
 
+static int rowgemm_kc2(int Kc) {
+  return Kc < 32 ? (Kc + 1) / 2 : ((Kc + 1) / 2 + 15) / 16 * 16;
+}
+
 bool rowgemm_ok(int Kc, int lda, int Nc) {
-  const int KC2 = ((Kc + 1) / 2 + 15) / 16 * 16;
+  const int KC2 = rowgemm_kc2(Kc);
   const int NT = (Nc + 31) / 32;
-  return Kc >= 2 && Kc <= 256 && Nc >= 1 && NT <= 8 && lda % 4 == 0 &&
+  return Kc >= 2 && Kc <= 256 && Nc >= 1 && NT <= 8 && lda >= Kc &&
          size_t(2) * KC2 * NT * 32 * 4 <= size_t(64) * 1024;
 }
 
 hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
                           int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
-                          int64_t c_plane, hipStream_t s, const float* res, int act) {
-  RowGemmArgs a{A, R, Kc, lda, ((Kc + 1) / 2 + 15) / 16 * 16, B, bs_k, bs_j, bs_p, Nc, C, ldc, c_plane,
-                res, act};
+                          int64_t c_plane, hipStream_t s, const float* res, int act, int pfin) {
+  if (pfin > 0 && (planes != 1 || res || act)) return hipErrorInvalidValue;
+  RowGemmArgs a{A, R, Kc, lda, rowgemm_kc2(Kc), B, bs_k, bs_j, bs_p, Nc, C, ldc, c_plane,
+                res, act, pfin,
+                int(lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0)};
   const int NT = (Nc + 31) / 32;
   const size_t lds = size_t(2) * a.KC2 * NT * 32 * 4;
   const int64_t ntiles = (R + 127) / 128;

@@ -57,7 +57,9 @@ enum {
 enum {
   CG_VARIANT_AUTO = 0,       /* fastest kernels that fit (cheb_fast when it applies)  */
   CG_VARIANT_CLASSIC = 1,    /* classic resident kernels (cheb_resident)              */
-  CG_VARIANT_UNFUSED_DW = 2  /* fast kernels, dW by the separate streaming GEMM       */
+  CG_VARIANT_UNFUSED_DW = 2, /* fast kernels, dW by the separate streaming GEMM       */
+  CG_VARIANT_NARROW = 3      /* streaming path in the sample-major layout even where
+                                the wide-column layout (Fin < 8) would apply          */
 };
 
 typedef struct cg_plan cg_plan;

@@ -49,9 +49,9 @@ def alg_bytes(M, nnz, B, K):
     return (K - 1) * csr + 4 * M * B * (2 + 3 * (K - 2)), (K - 1) * csr + 4 * M * B * (3 + 5 * (K - 2))
 
 
-def filter_config(name, Lt, N, Fin, K, Fout, dev):
+def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto"):
     M = Lt.shape[0]
-    plan = ChebPlan(Lt, device=0)
+    plan = ChebPlan(Lt, device=0, variant=variant)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
     x = torch.rand((N, M, Fin), device=dev, generator=g)
@@ -66,7 +66,7 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev):
     b = ev_ms(lambda: r.backward(dy, W), reps)
     bf, bb = alg_bytes(M, plan.nnz, N * Fin, K)
     return {"config": name, "M": M, "nnz": plan.nnz, "N": N, "Fin": Fin, "K": K, "Fout": Fout,
-            "path": r.path, "fwd_ms": round(f, 4), "bwd_ms": round(b, 4),
+            "path": r.path, "variant": variant, "fwd_ms": round(f, 4), "bwd_ms": round(b, 4),
             "samples_per_s": round(N / ((f + b) * 1e-3), 1),
             "fwd_alg_GBps": round(bf / (f * 1e-3) / 1e9, 1),
             "bwd_alg_GBps": round(bb / (b * 1e-3) / 1e9, 1)}
@@ -107,6 +107,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["C1", "C2", "D", "E"])
     ap.add_argument("--d-batch", type=int, default=32)
+    ap.add_argument("--variant", default="auto", help="plan variant (auto / narrow / ...)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -117,11 +118,11 @@ def main():
                 M = int(z["M"])
                 Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
             Fin = 1 if name == "C1" else 32
-            out = filter_config(name, Lt, 128, Fin, 5, 32, dev)
+            out = filter_config(name, Lt, 128, Fin, 5, 32, dev, args.variant)
         elif name == "D":
             import synth_graphs
             Lt = rescale_L(synth_graphs.config_d_laplacian(), 2)
-            out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev)
+            out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev, args.variant)
         elif name == "E":
             out = lstm_config(dev)
         else:

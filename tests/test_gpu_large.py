@@ -79,6 +79,46 @@ def test_config_c_golden(dev, graph_c, prefix):
     assert O.normwise_err(dW.cpu().numpy(), c["dW_ref"]) < TOL
 
 
+@pytest.mark.parametrize("N,Fin,K,Fout", [(128, 1, 5, 32), (64, 2, 5, 16), (48, 1, 3, 8),
+                                          (32, 1, 4, 40)])
+def test_config_c_wide_vs_narrow_layout(dev, graph_c, N, Fin, K, Fout):
+    """Config C layer 1 (Fin < 8) on the wide-column streaming layout
+    (cheb_wide.hip, [M][Fin*N]; B % 128 == 0: 8 XCD column groups, else one;
+    Fout % 8 == 0 and <= 32: the fused dy pass, else the row-GEMM planes)
+    vs the sample-major layout (variant 'narrow'): both vs the oracle incl.
+    the dx accumulation of the residual block's backward; the forward
+    (basis, y) bitwise equal between the layouts."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    rp, ci, v, M = graph_c["Lt_rowptr"], graph_c["Lt_col"], graph_c["Lt_val"], graph_c["M"]
+    rng = np.random.default_rng(3 * N + Fin)
+    x = rng.random((N, M, Fin), dtype=np.float32)
+    W = (rng.standard_normal((Fin * K, Fout)) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((N, M, Fout)).astype(np.float32)
+    dx0 = rng.standard_normal((N, M, Fin)).astype(np.float32)
+    out = {}
+    for variant in ("auto", "narrow"):
+        plan = ChebPlan(scipy.sparse.csr_matrix((v, ci, rp), shape=(M, M)), device=0, variant=variant)
+        assert plan.query_path(N, Fin, K, Fout) == "stream"
+        basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), K)
+        dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), K)
+        dxa = t(dx0, dev)
+        ops.cheb_backward_ex(plan, t(dy, dev), None, "none", basis, t(W, dev), K, dx=dxa,
+                             dx_accumulate=True)
+        torch.cuda.synchronize()
+        out[variant] = [a.cpu().numpy() for a in (basis, y, dx, dW, dxa)]
+    ob, oy = O.cheb_forward(x, rp, ci, v, W, K)
+    odx, odW = O.cheb_backward(dy, ob, W, rp, ci, v, N, M, Fin, K)
+    for variant, (basis, y, dx, dW, dxa) in out.items():
+        assert np.array_equal(basis, ob), variant
+        assert O.normwise_err(y, oy) < TOL, variant
+        assert O.normwise_err(dx, odx) < TOL, variant
+        assert O.normwise_err(dW, odW) < TOL, variant
+        assert O.normwise_err(dxa, odx + dx0) < TOL, variant
+    for a, b in zip(out["auto"][:2], out["narrow"][:2]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("N,Fin,K,Fout", [(128, 1, 5, 32), (8, 32, 5, 32)])
 def test_config_c_batch_vs_oracle(dev, graph_c, N, Fin, K, Fout):
     """Config C layer 1 at its full batch (N=128) and a layer-2 shape (Fin=32)."""
