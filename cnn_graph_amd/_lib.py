@@ -81,6 +81,9 @@ _SIGNATURES = {
                              _c_int),
     "cg_lstm_cell_backward": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
                               _c_int),
+    "cg_lstm_hconv_supported": ([_vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32)], _c_int),
+    "cg_lstm_hconv_step": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                            _vp, _vp, _c_i64, _vp], _c_int),
     "cg_perm_gather": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
     "cg_maxpool_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp], _c_int),
     "cg_maxpool_backward": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),

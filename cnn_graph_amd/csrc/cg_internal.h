@@ -281,6 +281,17 @@ hipError_t launch_lstm_bwd(int gates, int64_t R, int H, const float* dh, const f
                            const float* dc,
                            const float* act, const float* c, const float* c_out, float* dpre,
                            float* dc_prev, hipStream_t s);
+// One time step's h path of the gconv-LSTM in one launch (lstm_fused.hip):
+// the Chebyshev basis of h_prev in LDS, gh = basis Wh on MFMA, the gate
+// update; planes (nullable) receive T_1..T_{K-1} of h_prev ([N][M][H] each,
+// `plane` floats apart).  H == 32, M <= 1024.
+size_t lstm_hstep_lds(int M, int K);
+bool lstm_hstep_ok(int M, int H, int K);
+hipError_t launch_lstm_hstep(int gates, int N, int M, int K, const int* rowptr, const int* col,
+                             const float* val, const float* h_prev, const float* c_prev,
+                             const float* gx, const float* Wh, const float* bias, float* c_out,
+                             float* h_out, float* act, float* planes, int64_t plane,
+                             hipStream_t s);
 // Column sums of A [R][C] as [colsum_chunks(R)][C] partial slabs.
 int colsum_chunks(int64_t R);
 hipError_t launch_colsum_slabs(const float* A, int64_t R, int C, float* slab, hipStream_t s);

@@ -680,7 +680,8 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
                   const cg::AdamStep* adam = nullptr) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
-  if (!dy || !basis || !W) return fail(CG_ERR_ARG, "null dy/basis/W");
+  if (!dy || !W) return fail(CG_ERR_ARG, "null dy/W");
+  if (!basis && dW) return fail(CG_ERR_ARG, "null basis: dW needs the forward's basis");
   if (!dx && !dW) return fail(CG_ERR_ARG, "dx and dW are both NULL: nothing to compute");
   if ((rc = check_device(plan))) return rc;
   int path = 0;
@@ -1161,6 +1162,38 @@ int cg_lstm_cell_backward(int64_t R, int32_t H, int32_t gates, const float* dh,
   if (!act || !c_out || !dpre) return fail(CG_ERR_ARG, "lstm_cell_backward: null act/c_out/dpre");
   CG_HIP(cg::launch_lstm_bwd(gates, R, H, dh, dh_rec, dc, act, c, c_out, dpre, dc_prev,
                              reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_lstm_hconv_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* supported) {
+  if (!plan || !supported) return fail(CG_ERR_ARG, "lstm_hconv_supported: null argument");
+  *supported = cg::lstm_hstep_ok(plan->M, H, K) ? 1 : 0;
+  return ok();
+}
+
+int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates,
+                       const float* h_prev, const float* c_prev, const float* gx, const float* Wh,
+                       const float* bias, float* c_out, float* h_out, float* act, float* planes,
+                       int64_t plane_stride, void* stream) {
+  int rc = check_lstm(int64_t(N) * (plan ? plan->M : 1), H, gates);
+  if (rc) return rc;
+  if (!plan || N < 1 || K < 1) return fail(CG_ERR_ARG, "lstm_hconv_step: bad plan / N / K");
+  if (!h_prev || !gx || !Wh || !c_out || !h_out)
+    return fail(CG_ERR_ARG, "lstm_hconv_step: null h_prev / gx / Wh / c_out / h_out");
+  if (!cg::lstm_hstep_ok(plan->M, H, K))
+    return fail(CG_ERR_UNSUPPORTED, "lstm_hconv_step: needs H = 32, M <= 1024 and the LDS for K "
+                                    "(M=%d H=%d K=%d)", plan->M, H, K);
+  if (planes && K > 1 && plane_stride < int64_t(N) * plan->M * H)
+    return fail(CG_ERR_ARG, "lstm_hconv_step: plane stride %lld < N*M*H", (long long)plane_stride);
+  const void* outs[] = {c_out, h_out, act, planes};
+  const void* ins[] = {h_prev, c_prev, gx};
+  for (const void* o : outs)
+    for (const void* i : ins)
+      if (o && o == i) return fail(CG_ERR_ARG, "lstm_hconv_step: outputs must not alias inputs");
+  if ((rc = check_device(plan))) return rc;
+  CG_HIP(cg::launch_lstm_hstep(gates, N, plan->M, K, plan->rowptr, plan->col, plan->val, h_prev,
+                               c_prev, gx, Wh, bias, c_out, h_out, act, planes, plane_stride,
+                               reinterpret_cast<hipStream_t>(stream)));
   return ok();
 }
 

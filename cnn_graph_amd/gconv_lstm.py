@@ -16,12 +16,16 @@ Reference behaviour kept:
     ``static_rnn`` callers' own dropout if needed).
 
 MI355X design: the four x-weights (and the four h-weights) are stored
-concatenated as one [K*F, 4H] matrix, so a cell step is TWO chebyshev5 calls
-(one Chebyshev basis of x, one of h) plus one fused pointwise kernel, not the
-reference's eight filters.  ``static_rnn`` additionally batches the x-conv of
-ALL time steps into one call (it does not depend on the recurrence), runs the
-T h-convs back to back, and in the backward sums the h-weight gradient of all
-steps with one ``cg_weight_grad`` over the stacked bases.
+concatenated as one [K*F, 4H] matrix, so a cell step is ONE x-conv plus ONE
+h-step, not the reference's eight filters.  With H = 32 on graphs of up to
+1024 vertices (config E) the h-step is a single launch
+(``cg_lstm_hconv_step``): the Chebyshev basis of h in LDS, the gate
+contraction on MFMA and the gate update in its epilogue (``hconv="fused"``);
+otherwise it is a chebyshev5 call plus the pointwise kernel.  ``static_rnn``
+additionally batches the x-conv of ALL time steps into one call (it does not
+depend on the recurrence), runs the T h-steps back to back, and in the
+backward sums the h-weight gradient of all steps per Chebyshev order with one
+``cg_weight_grad`` over the stacked steps.
 """
 from __future__ import annotations
 
@@ -58,7 +62,8 @@ class GConvLSTMCell:
 
     def __init__(self, num_units, forget_bias=1.0, state_is_tuple=True, activation=None,
                  reuse=None, laplacian=None, lmax=None, K=None, feat_in=None, nNode=None,
-                 filter_type="cheby_conv", gates="reference", device=None, generator=None):
+                 filter_type="cheby_conv", gates="reference", device=None, generator=None,
+                 hconv="auto"):
         if filter_type != "cheby_conv":
             raise NotImplementedError(f"filter_type={filter_type!r}: only the Chebyshev filter "
                                       "is on the MI355X path (fourier_conv is out of scope)")
@@ -88,6 +93,14 @@ class GConvLSTMCell:
         self.Wx = torch.nn.Parameter(Wx)
         self.Wh = torch.nn.Parameter(Wh)
         self.b = torch.nn.Parameter(b)
+        # h path of a step: "fused" = cg_lstm_hconv_step (one launch), "unfused"
+        # = chebyshev5 + pointwise kernel; "auto" picks fused where it applies
+        if hconv not in ("auto", "fused", "unfused"):
+            raise ValueError("hconv must be 'auto', 'fused' or 'unfused'")
+        supported = ops.lstm_hconv_supported(self.plan, H, self._K)
+        if hconv == "fused" and not supported:
+            raise ValueError(f"hconv='fused' needs H = 32 and M <= 1024 (H={H}, M={self.plan.M})")
+        self.fused = supported and hconv != "unfused"
 
     # -- reference properties ---------------------------------------------------
     @property
@@ -144,24 +157,58 @@ class _CellStep(torch.autograd.Function):
         plan = cell.plan
         x, c, h = x.contiguous(), c.contiguous(), h.contiguous()
         basis_x, gx = ops.cheb_forward(plan, x, Wx, K)
-        basis_h, gh = ops.cheb_forward(plan, h, Wh, K)
-        c_out, h_out, act = ops.lstm_cell_forward(gx, gh, b, c, H, cell.gates)
-        ctx.save_for_backward(basis_x, basis_h, Wx, Wh, act, c, c_out)
+        if cell.fused:
+            N, M, _ = h.shape
+            planes = torch.empty((max(K - 1, 1), N * M, H), device=h.device, dtype=torch.float32)
+            c_out, h_out, act = ops.lstm_hconv_step(plan, h, c, gx, Wh, b, K, cell.gates,
+                                                    planes=planes[0], plane_stride=N * M * H)
+            ctx.save_for_backward(basis_x, planes, h, Wx, Wh, act, c, c_out)
+        else:
+            basis_h, gh = ops.cheb_forward(plan, h, Wh, K)
+            c_out, h_out, act = ops.lstm_cell_forward(gx, gh, b, c, H, cell.gates)
+            ctx.save_for_backward(basis_x, basis_h, h, Wx, Wh, act, c, c_out)
         ctx.cell = cell
         return c_out, h_out
 
     @staticmethod
     def backward(ctx, dc_out, dh_out):
-        basis_x, basis_h, Wx, Wh, act, c, c_out = ctx.saved_tensors
+        basis_x, hb, h, Wx, Wh, act, c, c_out = ctx.saved_tensors
         cell = ctx.cell
         H, K, plan = cell._num_units, cell._K, cell.plan
         dh = dh_out.contiguous() if dh_out is not None else None
         dc = dc_out.contiguous() if dc_out is not None else None
         dpre, dc_prev = ops.lstm_cell_backward(dh, None, dc, act, c, c_out, H, cell.gates)
         dx, dWx = ops.cheb_backward(plan, dpre, basis_x, Wx, K, need_dx=ctx.needs_input_grad[0])
-        dh_prev, dWh = ops.cheb_backward(plan, dpre, basis_h, Wh, K)
+        if cell.fused:
+            dh_prev, _ = ops.cheb_backward(plan, dpre, None, Wh, K, need_dW=False)
+            dWh = _hweight_grad_planes([h.view(-1, H)], [hb[k] for k in range(K - 1)], [dpre], H, K)
+        else:
+            dh_prev, dWh = ops.cheb_backward(plan, dpre, hb, Wh, K)
         db = ops.bias_grad(dpre)
         return dx, dc_prev, dh_prev, dWx, dWh, db, None
+
+
+def _hweight_grad_planes(t0_parts, planes, dpre_parts, H: int, K: int):
+    """dWh [K*H, 4H] (row c*K + k) from the Chebyshev orders of h kept as
+    planes: order 0 is h itself, given as row blocks t0_parts matched with
+    dpre_parts (summed with one cg_weight_grad each, accumulated); order k >= 1
+    is planes[k-1] (rows matching the concatenation of dpre_parts)."""
+    dev = dpre_parts[0].device
+    tmp = torch.empty((K, H, 4 * H), device=dev, dtype=torch.float32)
+    for i, (a, d) in enumerate(zip(t0_parts, dpre_parts)):
+        ops.weight_grad(a, d, out=tmp[0], accumulate=i > 0)
+    dcat = dpre_parts[0] if len(dpre_parts) == 1 else None
+    for k in range(1, K):
+        if dcat is not None:
+            ops.weight_grad(planes[k - 1], dcat, out=tmp[k])
+        else:  # the planes' rows follow the concatenation of dpre_parts
+            off = 0
+            for i, d in enumerate(dpre_parts):
+                rows = d.numel() // (4 * H)
+                ops.weight_grad(planes[k - 1].reshape(-1, H)[off:off + rows], d, out=tmp[k],
+                                accumulate=i > 0)
+                off += rows
+    return tmp.permute(1, 0, 2).reshape(K * H, 4 * H)
 
 
 class _Layer(torch.autograd.Function):
@@ -182,23 +229,32 @@ class _Layer(torch.autograd.Function):
         hs = torch.empty((T, N, M, H), **f32)
         cs = torch.empty((T, N, M, H), **f32)
         act = torch.empty((T, R, 4 * H), **f32)
-        basis_h = torch.empty((T, R, H * K), **f32)
-        gh = torch.empty((N, M, 4 * H), **f32)
+        fused = cell.fused
+        # h bases kept for the backward's weight gradient: the fused h-step
+        # writes the orders 1..K-1 as planes [K-1][T][R][H] (order 0 is h_prev)
+        planes = torch.empty((max(K - 1, 1), T, R, H), **f32) if fused else None
+        basis_h = None if fused else torch.empty((T, R, H * K), **f32)
+        gh = None if fused else torch.empty((N, M, 4 * H), **f32)
         for t in range(T):
             h_prev = (None if zero_init else h0) if t == 0 else hs[t - 1]
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
+            if h_prev is not None and fused:  # one launch: h-conv + gates
+                ops.lstm_hconv_step(plan, h_prev, c_prev, gx[t], Wh, b, K, gates, out_c=cs[t],
+                                    out_h=hs[t], out_act=act[t], planes=planes[0, t],
+                                    plane_stride=T * R * H)
+                continue
             if h_prev is not None:
                 ops.cheb_forward(plan, h_prev, Wh, K, out_basis=basis_h[t], out_y=gh)
             ops.lstm_cell_forward(gx[t], gh if h_prev is not None else None, b, c_prev, H, gates,
                                   out_c=cs[t], out_h=hs[t], out_act=act[t])
-        ctx.save_for_backward(basis_x, basis_h, Wx, Wh, act, cs, c0, h0)
-        ctx.cell, ctx.zero_init, ctx.shape = cell, zero_init, (T, N, M, F)
+        ctx.save_for_backward(basis_x, planes if fused else basis_h, Wx, Wh, act, cs, c0, h0, hs)
+        ctx.cell, ctx.zero_init, ctx.shape, ctx.fused = cell, zero_init, (T, N, M, F), fused
         return hs, cs[T - 1].clone()
 
     @staticmethod
     def backward(ctx, dhs, dcT):
-        basis_x, basis_h, Wx, Wh, act, cs, c0, _h0 = ctx.saved_tensors
-        cell, zero_init = ctx.cell, ctx.zero_init
+        basis_x, hb, Wx, Wh, act, cs, c0, h0, hs = ctx.saved_tensors
+        cell, zero_init, fused = ctx.cell, ctx.zero_init, ctx.fused
         H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
         T, N, M, F = ctx.shape
         R = N * M
@@ -214,11 +270,24 @@ class _Layer(torch.autograd.Function):
                                                 c_prev, cs[t], H, gates, out_dpre=dpre[t])
             if t >= t_first:
                 dh_rec, _ = ops.cheb_backward(plan, dpre[t].view(N, M, 4 * H),
-                                              basis_h[t].view(R, H * K), Wh, K, need_dW=False)
+                                              None if fused else hb[t].view(R, H * K), Wh, K,
+                                              need_dW=False)
             else:
                 dh_rec = None
-        dWh = (ops.weight_grad(basis_h[t_first:], dpre[t_first:]) if T > t_first
-               else torch.zeros_like(Wh))
+        if T <= t_first:
+            dWh = torch.zeros_like(Wh)
+        elif fused:
+            t0_parts, dparts = [], []
+            if t_first == 0:  # step 0 ran its h-conv on h0
+                t0_parts.append(h0.reshape(R, H))
+                dparts.append(dpre[0])
+            if T > 1:
+                t0_parts.append(hs[0:T - 1].reshape(-1, H))
+                dparts.append(dpre[1:T])
+            dWh = _hweight_grad_planes(t0_parts, [hb[k, t_first:T] for k in range(K - 1)], dparts,
+                                       H, K)
+        else:
+            dWh = ops.weight_grad(hb[t_first:], dpre[t_first:])
         dxs, dWx = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), basis_x, Wx, K,
                                      need_dx=ctx.needs_input_grad[0])
         db = ops.bias_grad(dpre)

@@ -420,6 +420,51 @@ def lstm_cell_forward(gx, gh, bias, c, H: int, gates="reference", out_c=None, ou
     return c_out, h_out, act
 
 
+def lstm_hconv_supported(plan: ChebPlan, H: int, K: int) -> bool:
+    """Whether cg_lstm_hconv_step serves this graph / hidden size / order."""
+    ok = ctypes.c_int32()
+    _lib.call("cg_lstm_hconv_supported", plan.handle, int(H), int(K), ctypes.byref(ok))
+    return bool(ok.value)
+
+
+def lstm_hconv_step(plan: ChebPlan, h_prev, c_prev, gx, Wh, bias, K: int, gates="reference",
+                    out_c=None, out_h=None, out_act=None, planes=None, plane_stride: int = 0):
+    """One time step of GConvLSTMCell's h path in one launch (cg_lstm_hconv_step):
+    the Chebyshev basis of h_prev, gh = basis Wh on MFMA and the gate update,
+    given the step's x-conv gx [..., 4H].  planes (optional, a tensor whose
+    storage holds K-1 planes [N, M, H] plane_stride floats apart) receives
+    T_1 .. T_{K-1} of h_prev.  Returns (c', h', act)."""
+    _check_dev("h_prev", h_prev)
+    h_prev = h_prev.contiguous()
+    N, M, H = (int(v) for v in h_prev.shape)
+    R = N * M
+    dev = h_prev.device
+    for name, t, n in (("gx", gx, 4 * H), ("c_prev", c_prev, H), ("bias", bias, 4 * H)):
+        if t is not None:
+            _check_dev(name, t)
+            if not t.is_contiguous() or t.numel() != (n if name == "bias" else R * n):
+                raise ValueError(f"{name}: bad shape {tuple(t.shape)}")
+    if tuple(Wh.shape) != (K * H, 4 * H) or not Wh.is_contiguous():
+        raise ValueError(f"Wh must be a contiguous [{K * H}, {4 * H}] tensor")
+    c_out = out_c if out_c is not None else torch.empty((N, M, H), device=dev, dtype=torch.float32)
+    h_out = out_h if out_h is not None else torch.empty((N, M, H), device=dev, dtype=torch.float32)
+    act = out_act if out_act is not None else torch.empty((N, M, 4 * H), device=dev,
+                                                          dtype=torch.float32)
+    _check_out("c_out", c_out, (R, H))
+    _check_out("h_out", h_out, (R, H))
+    _check_out("act", act, (R, 4 * H))
+    if planes is not None:
+        _check_dev("planes", planes)
+        need = (K - 2) * plane_stride + R * H if K > 1 else 0
+        avail = planes.untyped_storage().nbytes() // 4 - planes.storage_offset()
+        if K > 1 and (plane_stride < R * H or avail < need):
+            raise ValueError("planes: storage too small for the K-1 planes at this stride")
+    _lib.call("cg_lstm_hconv_step", plan.handle, N, H, int(K), LSTM_GATES[gates], _p(h_prev),
+              _p(c_prev), _p(gx), _p(Wh), _p(bias), _p(c_out), _p(h_out), _p(act), _p(planes),
+              int(plane_stride), _stream(h_prev))
+    return c_out, h_out, act
+
+
 def lstm_cell_backward(dh, dh_rec, dc, act, c, c_out, H: int, gates="reference", out_dpre=None,
                        need_dc_prev=True):
     """Backward of lstm_cell_forward: (dpre [..., 4H], dc_prev [..., H] or None)."""

@@ -256,6 +256,22 @@ int cg_lstm_cell_backward(int64_t R, int32_t H, int32_t gates, const float* dh,
                           const float* act, const float* c, const float* c_out, float* dpre,
                           float* dc_prev, void* stream);
 
+/* One time step of the cell's h path in ONE launch (the four h-gate
+ * cheby_conv calls of GConvLSTMCell.__call__, lib/gconv_lstm.py:183-207, plus
+ * the pointwise update above): the Chebyshev basis of h_prev [N][M][H] is
+ * built in LDS, gh = basis Wh on MFMA (Wh [K*H][4H], row c*K + k -- the four
+ * gate weights concatenated), a = (gx + gh) + bias, then c_out, h_out, act as
+ * cg_lstm_cell_forward.  planes (NULL to skip) receives T_1 .. T_{K-1} of
+ * h_prev, plane k-1 at planes + (k-1)*plane_stride, each [N][M][H] (the
+ * backward's weight gradient reads them).  c_prev / bias may be NULL (zero).
+ * Needs H == 32, M <= 1024 and the LDS of K (cg_lstm_hconv_supported);
+ * replaces cg_cheb_forward(h) + cg_lstm_cell_forward for one step. */
+int cg_lstm_hconv_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* supported);
+int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates,
+                       const float* h_prev, const float* c_prev, const float* gx, const float* Wh,
+                       const float* bias, float* c_out, float* h_out, float* act, float* planes,
+                       int64_t plane_stride, void* stream);
+
 /* ---------------------------------------------------------------------------
  * perm_data (lib/coarsening.py:219-240) on device:
  *   out[n][i][f] = perm[i] < M_in ? x[n][perm[i]][f] : 0   (fake vertices are 0)

@@ -72,14 +72,14 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto"):
             "bwd_alg_GBps": round(bb / (b * 1e-3) / 1e9, 1)}
 
 
-def lstm_config(dev, T=12, N=128, Fin=2, H=32, K=3):
+def lstm_config(dev, T=12, N=128, Fin=2, H=32, K=3, hconv="auto"):
     from cnn_graph_amd.gconv_lstm import GConvLSTMCell, layer
     with np.load(os.path.join(ROOT, "tests", "golden", "golden_E.npz"), allow_pickle=False) as z:
         M = int(z["M"])
         Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
     # L = L~ + I  (rescale_L(L, 2) = L - I gives back this L~)
     L = (Lt + scipy.sparse.identity(M, dtype=np.float32, format="csr")).tocsr()
-    cell = GConvLSTMCell(H, laplacian=L, lmax=2, K=K, feat_in=Fin, device=dev)
+    cell = GConvLSTMCell(H, laplacian=L, lmax=2, K=K, feat_in=Fin, device=dev, hconv=hconv)
     M = L.shape[0]
     g = torch.Generator(device=dev)
     g.manual_seed(2)
@@ -98,7 +98,8 @@ def lstm_config(dev, T=12, N=128, Fin=2, H=32, K=3):
     torch.cuda.synchronize()
     f = ev_ms(fwd, 3)
     fb = ev_ms(fwdbwd, 3)
-    return {"config": "E", "M": M, "T": T, "N": N, "Fin": Fin, "H": H, "K": K,
+    return {"config": "E", "hconv": "fused" if cell.fused else "unfused",
+            "M": M, "T": T, "N": N, "Fin": Fin, "H": H, "K": K,
             "fwd_ms": round(f, 3), "fwd_bwd_ms": round(fb, 3),
             "samples_per_s": round(N / (fb * 1e-3), 1)}
 
@@ -125,6 +126,8 @@ def main():
             out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev, args.variant)
         elif name == "E":
             out = lstm_config(dev)
+        elif name == "E_unfused":
+            out = lstm_config(dev, hconv="unfused")
         else:
             raise SystemExit(f"unknown config {name}")
         print(json.dumps(out), flush=True)

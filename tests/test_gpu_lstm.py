@@ -36,7 +36,7 @@ def graph_E():
     return Lt, (c["Lt_rowptr"], c["Lt_col"], c["Lt_val"].astype(np.float64)), M
 
 
-def make_cell(Lt, feat_in, H, K, gates, dev, seed):
+def make_cell(Lt, feat_in, H, K, gates, dev, seed, hconv="auto"):
     """A cell on L~ directly (lmax=2 rescale happens in plan_for, so hand it
     the plan of L~ by constructing from L = L~ + I: rescale_L(L, 2) = L~)."""
     from cnn_graph_amd.gconv_lstm import GConvLSTMCell
@@ -44,7 +44,7 @@ def make_cell(Lt, feat_in, H, K, gates, dev, seed):
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     cell = GConvLSTMCell(H, laplacian=L, lmax=2, K=K, feat_in=feat_in, gates=gates, device=dev,
-                         generator=g)
+                         generator=g, hconv=hconv)
     return cell, L
 
 
@@ -119,11 +119,14 @@ def test_weight_and_bias_grad_accumulate(dev):
 
 
 @pytest.mark.parametrize("gates", ["reference", "standard"])
-def test_cell_step_autograd_vs_oracle(dev, gates):
-    """GConvLSTMCell.__call__ with a non-zero state, gradients by autograd."""
+@pytest.mark.parametrize("H,K", [(8, 3), (32, 3), (32, 2), (32, 4)])
+def test_cell_step_autograd_vs_oracle(dev, gates, H, K):
+    """GConvLSTMCell.__call__ with a non-zero state, gradients by autograd
+    (H = 32: the one-launch h-step, cg_lstm_hconv_step)."""
     Lt, _, M = graph_E()
-    N, Fin, H, K = 3, 2, 8, 3
+    N, Fin = 3, 2
     cell, L = make_cell(Lt, Fin, H, K, gates, dev, seed=11)
+    assert cell.fused == (H == 32)
     lap = oracle_lap(cell, L)
     rng = np.random.default_rng(2)
     x, c0, h0 = rng.standard_normal((N, M, Fin)), rng.standard_normal((N, M, H)) * 0.5, \
@@ -148,12 +151,13 @@ def test_cell_step_autograd_vs_oracle(dev, gates):
 
 
 @pytest.mark.parametrize("zero_init", [True, False])
-def test_two_layer_static_rnn_vs_oracle(dev, zero_init):
+@pytest.mark.parametrize("H", [8, 32])
+def test_two_layer_static_rnn_vs_oracle(dev, zero_init, H):
     """static_rnn(MultiRNNCell([cell1, cell2])) (lib/gconv_lstm.py:609-627),
-    T=4, zero or given initial state, full BPTT."""
+    T=4, zero or given initial state, full BPTT (H = 32: fused h-steps)."""
     from cnn_graph_amd.gconv_lstm import static_rnn
     Lt, _, M = graph_E()
-    T, N, Fin, H, K = 4, 2, 2, 8, 3
+    T, N, Fin, K = 4, 2, 2, 3
     cell1, L = make_cell(Lt, Fin, H, K, "reference", dev, seed=21)
     cell2, _ = make_cell(Lt, H, H, K, "reference", dev, seed=22)
     lap = oracle_lap(cell1, L)
@@ -228,3 +232,28 @@ def test_config_E_sequence_path_equals_cell_steps(dev):
     f64 = lambda a: a.detach().cpu().numpy().astype(np.float64)  # noqa: E731
     h_ref, _, _ = LO.layer_forward(f64(xs[:, :n]), params_np(cell), lap, K, H)
     assert O.normwise_err(f64(hs[:, :n]), h_ref) < TOL
+
+
+def test_fused_hstep_equals_unfused(dev):
+    """The one-launch h-step (cg_lstm_hconv_step) against the chebyshev5 +
+    pointwise pair on config E's graph at N = 16 (the 2-workgroups-per-sample
+    XCD pairing): states, every gradient."""
+    from cnn_graph_amd.gconv_lstm import layer
+    Lt, _, M = graph_E()
+    T, N, Fin, H, K = 5, 16, 2, 32, 3
+    res = {}
+    for mode in ("fused", "unfused"):
+        cell, _ = make_cell(Lt, Fin, H, K, "reference", dev, seed=41, hconv=mode)
+        g = torch.Generator(device=dev)
+        g.manual_seed(3)
+        xs = torch.randn((T, N, M, Fin), device=dev, generator=g).requires_grad_()
+        gh = torch.randn((T, N, M, H), device=dev, generator=g)
+        c0 = (torch.randn((N, M, H), device=dev, generator=g) * 0.5).requires_grad_()
+        h0 = (torch.randn((N, M, H), device=dev, generator=g) * 0.5).requires_grad_()
+        hs, (cT, _) = layer(cell, xs, (c0, h0))
+        ((hs * gh).sum() + cT.sum()).backward()
+        torch.cuda.synchronize()
+        res[mode] = [hs.detach(), cT.detach(), xs.grad, c0.grad, h0.grad] + \
+            [p.grad for p in cell.parameters()]
+    for a, b in zip(res["fused"], res["unfused"]):
+        assert O.normwise_err(a.cpu().numpy(), b.cpu().numpy().astype(np.float64)) < 1e-5
