@@ -104,8 +104,9 @@ hipError_t launch_resident_backward(const ResidentGeom& g, int N, const Resident
 constexpr int kFastWidth = 16;  // register slots per row
 // Device image of a sparse operand for the fast kernels (built on the host by
 // cheb_abi.cpp::build_fast_image).  Thread t owns row[t] (-1 = idle); its
-// own ring record is rpos[t] and its CSR entries gather records cpos[j][t]
-// (j < 16, column-major; padding gathers the zero record zpos with val 0).
+// own ring record is rpos[t] and its CSR entries gather records
+// cpos[j/2][t] >> (16 * (j & 1)) & 0xffff (j < 16: two 16-bit record indices
+// per word, column-major; padding gathers the zero record zpos with val 0).
 // mpos[m] is the record of vertex m (m < 32*ceil(M/32); zpos past M);
 // wlen[w] the max row length of wave w.  Records: P (>= M + 2, incl. the zero
 // record and a dummy record that idle lanes write).

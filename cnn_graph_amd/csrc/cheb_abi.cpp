@@ -205,7 +205,15 @@ int build_fast_image(cg_plan::Fast* out, int32_t M, const int32_t* rp, const int
     if (r < 0) continue;
     for (int j = 0; j < rp[r + 1] - rp[r]; ++j) val[size_t(j) * kT + t] = v[rp[r] + j];
   }
-  const std::vector<int>* ints[] = {&lay.row, &lay.rpos0, &lay.rpos1, &lay.rposr, &lay.cpos,
+  // gather records packed two per word (record indices < 2^16): the per-thread
+  // image the fast kernels load in their prologue is 8 words smaller
+  if (lay.P >= 65536) return CG_OK;  // (never for M <= 1024: P ~ 2M + 66)
+  std::vector<int> cpos2(size_t(kWd / 2) * kT);
+  for (int j2 = 0; j2 < kWd / 2; ++j2)
+    for (int t = 0; t < kT; ++t)
+      cpos2[size_t(j2) * kT + t] = int(uint32_t(lay.cpos[size_t(2 * j2) * kT + t]) |
+                                       (uint32_t(lay.cpos[size_t(2 * j2 + 1) * kT + t]) << 16));
+  const std::vector<int>* ints[] = {&lay.row, &lay.rpos0, &lay.rpos1, &lay.rposr, &cpos2,
                                     &lay.wlen, &lay.mpos, &lay.pos0, &lay.pos1};
   size_t bytes = val.size() * 4;
   for (const auto* a : ints) bytes += a->size() * 4;
@@ -225,7 +233,7 @@ int build_fast_image(cg_plan::Fast* out, int32_t M, const int32_t* rp, const int
   e.rpos = static_cast<const int*>(put(lay.rpos0.data(), lay.rpos0.size()));
   e.rpos1 = static_cast<const int*>(put(lay.rpos1.data(), lay.rpos1.size()));
   e.rposr = static_cast<const int*>(put(lay.rposr.data(), lay.rposr.size()));
-  e.cpos = static_cast<const int*>(put(lay.cpos.data(), lay.cpos.size()));
+  e.cpos = static_cast<const int*>(put(cpos2.data(), cpos2.size()));
   e.val = static_cast<const float*>(put(val.data(), val.size()));
   e.wlen = static_cast<const int*>(put(lay.wlen.data(), lay.wlen.size()));
   e.mpos = static_cast<const int*>(put(lay.mpos.data(), lay.mpos.size()));

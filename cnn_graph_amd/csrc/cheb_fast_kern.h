@@ -141,10 +141,13 @@ struct Row {
     (void)wl;  // loading only the first wl slots was measured SLOWER (per-slot
                // branches serialise the loads): load all 16 unconditionally
 #pragma unroll
-    for (int j = 0; j < kFastWidth; ++j) {
-      ca[j] = E.cpos[j * kT + tid] * REC;
-      v[j] = E.val[j * kT + tid];
+    for (int j2 = 0; j2 < kFastWidth / 2; ++j2) {
+      const uint32_t pk = uint32_t(E.cpos[j2 * kT + tid]);
+      ca[2 * j2] = int(pk & 0xffffu) * REC;
+      ca[2 * j2 + 1] = int(pk >> 16) * REC;
     }
+#pragma unroll
+    for (int j = 0; j < kFastWidth; ++j) v[j] = E.val[j * kT + tid];
   }
 
   // sum_{j < L, CSR order} v_j * T[c_j][SLOT]  (sequential, one rounding each)
@@ -316,21 +319,8 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
     default: break;  // unreachable: the host only selects this kernel for rows <= 16
   }
 
-  if (c.keep_basis) {
-    __syncthreads();
-    float* basis_n = A.basis + size_t(n) * M * FinK;
-    const int total = M * FinK;
-    if ((reinterpret_cast<uintptr_t>(basis_n) & 15) == 0) {
-      const int n4 = total >> 2;
-      const float4* src = reinterpret_cast<const float4*>(c.s_B);
-      float4* dst = reinterpret_cast<float4*>(basis_n);
-      for (int i = tid; i < n4; i += kT) dst[i] = src[i];
-      for (int i = (n4 << 2) + tid; i < total; i += kT) basis_n[i] = c.s_B[i];
-    } else {
-      for (int i = tid; i < total; i += kT) basis_n[i] = c.s_B[i];
-    }
-  }
-
+  // y first: its stores leave from registers while the other waves finish
+  // the last pair; then the block-wide barrier for the basis staged in LDS
   if (A.y && !CG_DBG(A.dbg, 8)) {
     float* yn = A.y + size_t(n) * M * Fout;
 #pragma unroll
@@ -352,6 +342,21 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
           }
         }
       }
+    }
+  }
+
+  if (c.keep_basis) {
+    __syncthreads();
+    float* basis_n = A.basis + size_t(n) * M * FinK;
+    const int total = M * FinK;
+    if ((reinterpret_cast<uintptr_t>(basis_n) & 15) == 0) {
+      const int n4 = total >> 2;
+      const float4* src = reinterpret_cast<const float4*>(c.s_B);
+      float4* dst = reinterpret_cast<float4*>(basis_n);
+      for (int i = tid; i < n4; i += kT) dst[i] = src[i];
+      for (int i = (n4 << 2) + tid; i < total; i += kT) basis_n[i] = c.s_B[i];
+    } else {
+      for (int i = tid; i < total; i += kT) basis_n[i] = c.s_B[i];
     }
   }
 }
