@@ -199,6 +199,8 @@ def main():
     ap.add_argument("--global-batch", type=int, default=None,
                     help="fixed whole-job batch sharded over the ranks (strong scaling)")
     ap.add_argument("--path", default="auto", choices=["auto", "resident", "stream"])
+    ap.add_argument("--basis-layout", default="auto", choices=["auto", "rows", "orders"],
+                    help="saved-basis layout (orders where the fast kernels apply)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "torch"],
@@ -244,7 +246,9 @@ def main():
     m_adam = torch.zeros_like(W)
     v_adam = torch.zeros_like(W)
 
-    runner = ops.ChebRunner(plan, N, Fin, K, Fout, dev)
+    # the orders basis layout where the fast kernels apply (config B): the
+    # forward stores the basis during its recurrence (cg_cheb_basis_elems)
+    runner = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=args.basis_layout)
     stream = torch.cuda.current_stream(dev).cuda_stream
     adam = _lib.lib().cg_adam_update
     adam_args = (W.data_ptr(), runner.dW.data_ptr(), m_adam.data_ptr(), v_adam.data_ptr(),
@@ -338,7 +342,8 @@ def main():
         "config": {"workload": "config B: MNIST 8-NN grid coarsened, M=976, nnz=6396, K=25, Fin=1, "
                                "Fout=32, chebyshev5 fwd+bwd + dW all-reduce + Adam",
                    "batch_per_gpu": N, "global_batch": N_global, "M": M, "nnz": plan.nnz, "K": K,
-                   "Fin": Fin, "Fout": Fout, "path": path, "parallelism": f"dp{world}",
+                   "Fin": Fin, "Fout": Fout, "path": path, "basis_layout": runner.basis_layout,
+                   "parallelism": f"dp{world}",
                    "allreduce": (args.allreduce if exchange else None),
                    "adam": ("fused into the dW reduction (cg_cheb_backward_adam)" if fuse_adam
                             else "cg_adam_update")},

@@ -21,6 +21,8 @@ PATHS = {"auto": CG_PATH_AUTO, "resident": CG_PATH_RESIDENT, "stream": CG_PATH_S
 CG_VARIANT_AUTO, CG_VARIANT_CLASSIC, CG_VARIANT_UNFUSED_DW, CG_VARIANT_NARROW = 0, 1, 2, 3
 VARIANTS = {"auto": CG_VARIANT_AUTO, "classic": CG_VARIANT_CLASSIC,
             "unfused_dw": CG_VARIANT_UNFUSED_DW, "narrow": CG_VARIANT_NARROW}
+CG_BASIS_ROWS, CG_BASIS_ORDERS = 0, 1
+BASIS_LAYOUTS = {"rows": CG_BASIS_ROWS, "orders": CG_BASIS_ORDERS}
 
 
 class CGError(RuntimeError):
@@ -55,6 +57,16 @@ _SIGNATURES = {
                             _c_sz, _vp], _c_int),
     "cg_cheb_backward_ex": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp,
                              _c_i32, _vp, _vp, _vp, _c_sz, _vp], _c_int),
+    "cg_cheb_basis_elems": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64)],
+                            _c_int),
+    "cg_cheb_forward_layout": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _c_i32,
+                                _vp, _vp, _vp, _c_sz, _vp], _c_int),
+    "cg_cheb_backward_layout": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i32, _vp,
+                                 _vp, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp], _c_int),
+    "cg_cheb_backward_adam_layout": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp,
+                                      _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float,
+                                      ctypes.c_float, ctypes.c_float, _c_i32, ctypes.c_float, _vp,
+                                      _c_sz, _vp], _c_int),
     "cg_mse_loss_workspace_bytes": ([_c_i64, ctypes.POINTER(_c_sz)], _c_int),
     "cg_mse_loss": ([_vp, _vp, _c_i64, _vp, _vp, _vp, _c_sz, _vp], _c_int),
     "cg_mse_loss_ema": ([_vp, _vp, _c_i64, _vp, _vp, _vp, ctypes.c_float, _vp, _c_sz, _vp], _c_int),

@@ -33,10 +33,18 @@ inline int debug_flags() { return g_debug_flags; }
 // tuning overrides of the ablation build (cg_debug_set_param); -1 = default
 extern int g_debug_params[8];
 inline int debug_param(int i, int dflt) { return g_debug_params[i] >= 0 ? g_debug_params[i] : dflt; }
+// per-workgroup phase timestamps (cg_debug_set_ts): slot s of workgroup b at
+// ts[b * 8 + s], wall clock (s_memrealtime), written by thread 0
+extern unsigned long long* g_debug_ts;
+#define CG_TS(ts, slot)                                                              \
+  do {                                                                               \
+    if ((ts) && threadIdx.x == 0) (ts)[blockIdx.x * 8 + (slot)] = wall_clock64();    \
+  } while (0)
 #else
 constexpr int debug_param(int, int dflt) { return dflt; }
 #define CG_DBG(flags, bit) false
 constexpr int debug_flags() { return 0; }
+#define CG_TS(ts, slot) ((void)0)
 #endif
 
 // ---- resident (LDS) path ---------------------------------------------------
@@ -137,7 +145,8 @@ struct FastGeom {
   bool dw_fused;     // backward computes the dW partial in-kernel (FinK, Fout <= 32)
   size_t dscratch;   // bytes of the backward's dBasis / dW-reduce LDS region
   size_t fwd_lds, bwd_lds;
-  bool fwd_ok, bwd_ok;
+  size_t fwd_lds_ob;  // forward with the orders-layout basis (no LDS staging of it)
+  bool fwd_ok, bwd_ok, fwd_ok_ob;
 };
 FastGeom fast_geometry(int M, int P, int max_row_nnz, int max_row_nnzT, int Fin, int K, int Fout);
 struct FastFwdArgs {
@@ -149,6 +158,8 @@ struct FastFwdArgs {
   const float* W;
   float* basis;
   float* y;
+  int bord;  // 0: basis [N*M][Fin*K]; else the orders layout [N][Fin*K][bord] (bord = Mb)
+  unsigned long long* ts;  // ablation build: phase timestamps (CG_TS), else NULL
 };
 struct FastBwdArgs {
   int M, Fin, K, Fout, Mp, dbg;
@@ -160,6 +171,8 @@ struct FastBwdArgs {
   const float* W;
   float* dx;
   float* dw_slab;      // [N][FinK][Fout] per-sample dW partials, or NULL (no fused dW)
+  int bord;            // basis layout, as FastFwdArgs::bord
+  unsigned long long* ts;  // ablation build: phase timestamps (CG_TS), else NULL
 };
 hipError_t launch_fast_forward(const FastGeom& g, int N, const FastFwdArgs& a, hipStream_t s);
 hipError_t launch_fast_backward(const FastGeom& g, int N, const FastBwdArgs& a, hipStream_t s);

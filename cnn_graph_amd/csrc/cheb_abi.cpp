@@ -19,6 +19,7 @@
 namespace cg {
 int g_debug_flags = 0;
 int g_debug_params[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+unsigned long long* g_debug_ts = nullptr;
 }
 #endif
 
@@ -327,6 +328,26 @@ int choose_path(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, bool bac
 
 inline size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 
+// Basis layouts (cheb_mi355.h): CG_BASIS_ROWS [N*M][Fin*K] (lib/graph_conv.py:172)
+// on every path; CG_BASIS_ORDERS [N][Fin*K][Mb] (Mb = M rounded up to 32) where
+// the fast forward stores it during the recurrence and the fused-dW fast
+// backward reads it back.
+inline int32_t basis_mb(int32_t M) { return (M + 31) & ~31; }
+
+int check_layout(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, int layout) {
+  if (layout == CG_BASIS_ROWS) return CG_OK;
+  if (layout != CG_BASIS_ORDERS) return fail(CG_ERR_ARG, "unknown basis layout %d", layout);
+  // the fast forward without the basis staging (so it also serves shapes whose
+  // staged basis would not fit in LDS) and the fused-dW fast backward
+  if (Fin > 2 || p->path == CG_PATH_STREAM || p->variant == CG_VARIANT_CLASSIC || !p->fast.ok ||
+      !fast_geom(p, Fin, K, Fout).fwd_ok_ob || !fused_dw(p, Fin, K, Fout))
+    return fail(CG_ERR_UNSUPPORTED,
+                "orders basis layout needs Fin <= 2, the fast resident forward and the "
+                "fused-dW fast backward (M=%d Fin=%d K=%d Fout=%d)",
+                p->M, Fin, K, Fout);
+  return CG_OK;
+}
+
 struct StreamWs {
   bool wide;     // wide-column layout (cheb_wide.hip) for small Fin
   size_t slots;  // forward: T_1 .. T_{K-2} (sample-major), or the K planes T_0 .. T_{K-1} ([M][B], wide)
@@ -400,6 +421,12 @@ int cg_debug_set_flags(int flags) {
 }
 // Tuning override (ablation build only): launch code reads key k < 8 with
 // cg::debug_param(k, default); value -1 restores the default.
+// Phase timestamps of the fast kernels (ablation build only): a device buffer
+// of N * 8 uint64 or NULL.
+int cg_debug_set_ts(void* dev_buf) {
+  cg::g_debug_ts = static_cast<unsigned long long*>(dev_buf);
+  return ok();
+}
 int cg_debug_set_param(int key, int value) {
   if (key < 0 || key >= 8) return fail(CG_ERR_ARG, "bad debug param %d", key);
   cg::g_debug_params[key] = value;
@@ -576,9 +603,10 @@ namespace {
 // forward with the residual / activation epilogue y = act(basis W + res)
 int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout, const float* x,
                  const float* W, const float* res, int act, float* basis, float* y, void* workspace,
-                 size_t ws_bytes, void* stream) {
+                 size_t ws_bytes, void* stream, int layout = CG_BASIS_ROWS) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
+  if ((rc = check_layout(plan, Fin, K, Fout, layout))) return rc;
   if (!x) return fail(CG_ERR_ARG, "null x");
   if (act != CG_ACT_NONE && act != CG_ACT_RELU) return fail(CG_ERR_ARG, "unknown activation %d", act);
   if (!y && (res || act)) return fail(CG_ERR_ARG, "an epilogue needs y");
@@ -590,7 +618,7 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int M = plan->M;
 
-  if (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, false)) {
+  if (layout == CG_BASIS_ORDERS || (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, false))) {
     cg::FastFwdArgs a{};
     a.M = M;
     a.Fin = Fin;
@@ -604,6 +632,10 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
     a.y = y;
     a.res = res;
     a.act = act;
+    a.bord = layout == CG_BASIS_ORDERS ? basis_mb(M) : 0;
+#ifdef CG_DEBUG
+    a.ts = cg::g_debug_ts;
+#endif
     CG_HIP(cg::launch_fast_forward(fast_geom(plan, Fin, K, Fout), N, a, s));
     return ok();
   }
@@ -685,9 +717,12 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
 int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout, const float* dy,
                   const float* basis, const float* W, float* dx, int dx_acc, float* dW,
                   void* workspace, size_t ws_bytes, void* stream,
-                  const cg::AdamStep* adam = nullptr) {
+                  const cg::AdamStep* adam = nullptr, int layout = CG_BASIS_ROWS) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
+  if ((rc = check_layout(plan, Fin, K, Fout, layout))) return rc;
+  if (layout == CG_BASIS_ORDERS && dW && !dx)
+    return fail(CG_ERR_UNSUPPORTED, "orders basis layout: dW is fused into the dx pass (dx needed)");
   if (!dy || !W) return fail(CG_ERR_ARG, "null dy/W");
   if (!basis && dW) return fail(CG_ERR_ARG, "null basis: dW needs the forward's basis");
   if (!dx && !dW) return fail(CG_ERR_ARG, "dx and dW are both NULL: nothing to compute");
@@ -733,6 +768,10 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       a.dx = dx;
       a.dx_acc = dx_acc;
       a.dw_slab = fused ? slabs : nullptr;
+      a.bord = layout == CG_BASIS_ORDERS ? basis_mb(M) : 0;
+#ifdef CG_DEBUG
+      a.ts = cg::g_debug_ts;
+#endif
       CG_HIP(cg::launch_fast_backward(g, N, a, s));
     } else if (path == CG_PATH_RESIDENT) {
       const cg::ResidentGeom g = cg::resident_geometry(M, int(plan->nnz), plan->max_row_nnz,
@@ -852,11 +891,12 @@ int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t F
   return backward_impl(plan, N, Fin, K, Fout, dy, basis, W, dx, 0, dW, workspace, ws_bytes, stream);
 }
 
-int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
-                          const float* dy, const float* basis, float* W, float* dx, float* dW,
-                          float* m, float* v, float lr, float beta1, float beta2, float eps,
-                          int32_t step, float grad_scale, void* workspace, size_t ws_bytes,
-                          void* stream) {
+namespace {
+int backward_adam_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                       int layout, const float* dy, const float* basis, float* W, float* dx,
+                       float* dW, float* m, float* v, float lr, float beta1, float beta2,
+                       float eps, int32_t step, float grad_scale, void* workspace,
+                       size_t ws_bytes, void* stream) {
   if (!dW || !W || !m || !v || step < 1)
     return fail(CG_ERR_ARG, "cheb_backward_adam: dW, W, m, v required and step >= 1");
   // the reduction stores grad[i] and then updates param/m/v[i] in place:
@@ -879,15 +919,18 @@ int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int3
   a.eps = eps;
   a.grad_scale = grad_scale;
   return backward_impl(plan, N, Fin, K, Fout, dy, basis, W, dx, 0, dW, workspace, ws_bytes, stream,
-                       &a);
+                       &a, layout);
 }
 
-int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
-                        const float* dy, const float* y, int32_t act, const float* basis,
-                        const float* W, float* dx, int32_t dx_accumulate, float* dW, float* dz,
-                        void* workspace, size_t ws_bytes, void* stream) {
+int backward_ex_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                     const float* dy, const float* y, int32_t act, int layout, const float* basis,
+                     const float* W, float* dx, int32_t dx_accumulate, float* dW, float* dz,
+                     void* workspace, size_t ws_bytes, void* stream) {
   if (act != CG_ACT_NONE && act != CG_ACT_RELU) return fail(CG_ERR_ARG, "unknown activation %d", act);
   if (!plan || !dy) return fail(CG_ERR_ARG, "null plan / dy");
+  int rc = check_shape(plan, N, Fin, K, Fout);
+  if (rc) return rc;
+  if ((rc = check_layout(plan, Fin, K, Fout, layout))) return rc;
   const float* dy_eff = dy;
   if (act == CG_ACT_RELU) {
     if (!y || !dz) return fail(CG_ERR_ARG, "ReLU backward needs y (its output) and dz");
@@ -900,7 +943,61 @@ int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_
   }
   if (!dx && !dW) return ok();
   return backward_impl(plan, N, Fin, K, Fout, dy_eff, basis, W, dx, dx_accumulate != 0, dW,
-                       workspace, ws_bytes, stream);
+                       workspace, ws_bytes, stream, nullptr, layout);
+}
+}  // namespace
+
+int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                          const float* dy, const float* basis, float* W, float* dx, float* dW,
+                          float* m, float* v, float lr, float beta1, float beta2, float eps,
+                          int32_t step, float grad_scale, void* workspace, size_t ws_bytes,
+                          void* stream) {
+  return backward_adam_impl(plan, N, Fin, K, Fout, CG_BASIS_ROWS, dy, basis, W, dx, dW, m, v, lr,
+                            beta1, beta2, eps, step, grad_scale, workspace, ws_bytes, stream);
+}
+
+int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                        const float* dy, const float* y, int32_t act, const float* basis,
+                        const float* W, float* dx, int32_t dx_accumulate, float* dW, float* dz,
+                        void* workspace, size_t ws_bytes, void* stream) {
+  return backward_ex_impl(plan, N, Fin, K, Fout, dy, y, act, CG_BASIS_ROWS, basis, W, dx,
+                          dx_accumulate, dW, dz, workspace, ws_bytes, stream);
+}
+
+int cg_cheb_basis_elems(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                        int32_t layout, int64_t* elems) {
+  int rc = check_shape(plan, N, Fin, K, Fout);
+  if (rc) return rc;
+  if (!elems) return fail(CG_ERR_ARG, "null elems out-pointer");
+  if ((rc = check_layout(plan, Fin, K, Fout, layout))) return rc;
+  const int64_t rows = layout == CG_BASIS_ORDERS ? basis_mb(plan->M) : plan->M;
+  *elems = int64_t(N) * rows * Fin * K;
+  return ok();
+}
+
+int cg_cheb_forward_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                           const float* x, const float* W, const float* residual, int32_t act,
+                           int32_t layout, float* basis, float* y, void* workspace,
+                           size_t ws_bytes, void* stream) {
+  return forward_impl(plan, N, Fin, K, Fout, x, W, residual, act, basis, y, workspace, ws_bytes,
+                      stream, layout);
+}
+
+int cg_cheb_backward_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                            const float* dy, const float* y, int32_t act, int32_t layout,
+                            const float* basis, const float* W, float* dx, int32_t dx_accumulate,
+                            float* dW, float* dz, void* workspace, size_t ws_bytes, void* stream) {
+  return backward_ex_impl(plan, N, Fin, K, Fout, dy, y, act, layout, basis, W, dx, dx_accumulate,
+                          dW, dz, workspace, ws_bytes, stream);
+}
+
+int cg_cheb_backward_adam_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                                 int32_t layout, const float* dy, const float* basis, float* W,
+                                 float* dx, float* dW, float* m, float* v, float lr, float beta1,
+                                 float beta2, float eps, int32_t step, float grad_scale,
+                                 void* workspace, size_t ws_bytes, void* stream) {
+  return backward_adam_impl(plan, N, Fin, K, Fout, layout, dy, basis, W, dx, dW, m, v, lr, beta1,
+                            beta2, eps, step, grad_scale, workspace, ws_bytes, stream);
 }
 
 int cg_mse_loss_workspace_bytes(int64_t n, size_t* bytes) {

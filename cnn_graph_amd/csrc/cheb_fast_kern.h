@@ -167,7 +167,8 @@ struct Row {
 // ---------------------------------------------------------------------------
 // Forward
 // ---------------------------------------------------------------------------
-template <int FV, int NT>
+// OB: the basis goes out in the orders layout during the recurrence (no LDS staging)
+template <int FV, int NT, bool OB>
 struct Fwd {
   typedef typename VecT<FV>::type V;
   static constexpr int REC = 12 * FV;
@@ -177,14 +178,15 @@ struct Fwd {
   char* ring;
   float* s_W;
   float* s_B;
-  int K, M, Fout, FinK, wave, lane, li, h, ntiles;
+  float* gB;  // orders layout: this sample's [FinK][bord] basis planes in HBM
+  int K, M, Fout, FinK, wave, lane, li, h, ntiles, bord;
   int mb[MT];  // byte offsets of the records of this lane's MFMA tile rows
   bool keep_basis;
   Row r;
   V t1, t2;  // T_{k-1}, T_{k-2} of the own row
   f32x16 acc[MT][NT];
 
-  __device__ Fwd(const FastFwdArgs& a, char* smem, int tid) : A(a) {
+  __device__ __forceinline__ Fwd(const FastFwdArgs& a, char* smem, int tid) : A(a) {
     K = a.K;
     M = a.M;
     Fout = a.Fout;
@@ -200,9 +202,14 @@ struct Fwd {
     off = align16(off + size_t(FinK) * Fout * 4);
     s_B = reinterpret_cast<float*>(smem + off);
     keep_basis = a.basis != nullptr && !CG_DBG(a.dbg, 2);
+    bord = a.bord;
+    gB = a.basis ? a.basis + size_t(blockIdx.x) * FinK * bord : nullptr;
   }
 
-  // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA; stage the basis.
+  // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA; stage the basis
+  // (rows layout) or store it (orders layout: a half-wave's 32 rows of one
+  // order are 128 contiguous bytes, so each store is two whole lines and the
+  // basis leaves during the recurrence instead of after it).
   __device__ __forceinline__ void pair(int s) {
     const int kk = 2 * s + h;
     const bool kv = kk < K;
@@ -223,7 +230,10 @@ struct Fwd {
           float a = 0.f;
           if (kv) {
             a = lds_f(ring + mb[t] + soff + fin * 4);
-            if (keep_basis && m < M) s_B[m * FinK + fin * K + kk] = a;
+            if (keep_basis) {
+              if (OB) gB[(fin * K + kk) * bord + m] = a;  // rows >= M: the zero record
+              else if (m < M) s_B[m * FinK + fin * K + kk] = a;
+            }
           }
           if (!CG_DBG(A.dbg, 4)) {
 #pragma unroll
@@ -266,14 +276,15 @@ struct Fwd {
   }
 };
 
-template <int FV, int NT>
+template <int FV, int NT, bool OB>
 __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Fwd<FV, NT> F;
+  typedef Fwd<FV, NT, OB> F;
   constexpr int REC = F::REC;
   const int tid = threadIdx.x;
   const int n = blockIdx.x;
+  CG_TS(A.ts, 0);
   F c(A, smem, tid);
   const int M = c.M, Fout = c.Fout, FinK = c.FinK;
 
@@ -309,6 +320,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) c.acc[t][q][e] = 0.f;
   __syncthreads();
+  CG_TS(A.ts, 1);
   if (CG_DBG(A.dbg, 16)) return;
 
   switch (wl) {
@@ -318,6 +330,7 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 #undef CG_L
     default: break;  // unreachable: the host only selects this kernel for rows <= 16
   }
+  CG_TS(A.ts, 2);
 
   // y first: its stores leave from registers while the other waves finish
   // the last pair; then the block-wide barrier for the basis staged in LDS
@@ -345,7 +358,8 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
     }
   }
 
-  if (c.keep_basis) {
+  CG_TS(A.ts, 3);
+  if (!OB && c.keep_basis) {
     __syncthreads();
     float* basis_n = A.basis + size_t(n) * M * FinK;
     const int total = M * FinK;
@@ -359,21 +373,25 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
       for (int i = tid; i < total; i += kT) basis_n[i] = c.s_B[i];
     }
   }
+  CG_TS(A.ts, 4);
 }
 
 // ---------------------------------------------------------------------------
 // Backward: dBasis (phase A), Clenshaw over L~^T -> dx, fused dW partial
 // ---------------------------------------------------------------------------
-template <int FV, bool DW>
+// DW: 0 no fused dW, 1 fused dW from the rows-layout basis, 2 from the orders layout
+template <int FV, int DW>
 struct Bwd {
   typedef typename VecT<FV>::type V;
   static constexpr int REC = 12 * FV;
   static constexpr int NU = 2;  // dW MFMAs per recurrence step
+  static constexpr bool OB = DW == 2;
+  static_assert(NU == 2, "the orders-layout dW loads one row quad per step");
 
   const FastBwdArgs& A;
   char* ring;
   float* s_D;  // [FinK][Mp]
-  int K, M, Fout, FinK, Mp, wave, li, h, n;
+  int K, M, Fout, FinK, Mp, wave, li, h, n, bord;
   Row r;
   // fused dW: this wave's basis rows [dm0, dm1), 2 per MFMA
   int dm0, dm1, npair, nexti;
@@ -381,7 +399,7 @@ struct Bwd {
   f32x16 dacc;
   float da[3][NU], db[3][NU];
 
-  __device__ Bwd(const FastBwdArgs& a, char* smem, int tid) : A(a) {
+  __device__ __forceinline__ Bwd(const FastBwdArgs& a, char* smem, int tid) : A(a) {
     K = a.K;
     M = a.M;
     Fout = a.Fout;
@@ -394,13 +412,34 @@ struct Bwd {
     h = lane >> 5;
     ring = smem;
     s_D = reinterpret_cast<float*>(smem + align16(size_t(a.E.P) * REC));
+    bord = a.bord;
+  }
+
+  // Basis row of the wave's MFMA i in lane half h.  Rows layout: rows
+  // dm0 + 2i + h of the wave's chunk.  Orders layout: row quads dealt
+  // round-robin (quad w + 16g to wave w), MFMA 2g + u takes rows
+  // 4(w + 16g) + 2h + u: one 8-byte load per lane feeds both MFMAs of a
+  // step, and in a step the 16 waves read the same 256 contiguous bytes of
+  // each of the 32 planes (the lines are shared in L1 across the waves).
+  __device__ __forceinline__ int dw_row(int i) const {
+    return OB ? 4 * (wave + kW * (i >> 1)) + 2 * h + (i & 1) : dm0 + 2 * i + h;
   }
 
   // ---- fused dW: acc[j][f] += sum over row pairs of basis[m][j] * dy[m][f]
   __device__ __forceinline__ void dw_load(int buf, int i0) {
-    const float* bn = A.basis + size_t(n) * M * FinK;
     const float* dyn = A.dy + size_t(n) * M * Fout;
     const int jc = imin(li, FinK - 1), fc = imin(li, Fout - 1);
+    if (OB) {  // i0 even: rows dw_row(i0) + {0, 1}
+      const float* bn = A.basis + size_t(n) * FinK * bord;
+      const int m = dw_row(i0);
+      const float2 bv = *reinterpret_cast<const float2*>(bn + size_t(jc) * bord + imin(m, bord - 2));
+      da[buf][0] = bv.x;
+      da[buf][1] = bv.y;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) db[buf][u] = dyn[size_t(imin(m + u, M - 1)) * Fout + fc];
+      return;
+    }
+    const float* bn = A.basis + size_t(n) * M * FinK;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int m = imin(dm0 + 2 * (i0 + u) + h, M - 1);
@@ -413,7 +452,7 @@ struct Bwd {
     for (int u = 0; u < NU; ++u) {
       const int i = i0 + u;
       if (i < npair) {
-        const bool rv = dm0 + 2 * i + h < dm1;
+        const bool rv = dw_row(i) < dm1;
         dacc = mfma32((rv && li < FinK) ? da[buf][u] : 0.f, (rv && li < Fout) ? db[buf][u] : 0.f,
                       dacc);
       }
@@ -467,13 +506,14 @@ struct Bwd {
   }
 };
 
-template <int FV, bool DW>
+template <int FV, int DW>
 __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef Bwd<FV, DW> B;
   constexpr int REC = B::REC;
   const int tid = threadIdx.x;
+  CG_TS(A.ts, 0);
   B c(A, smem, tid);
   const int M = c.M, Fout = c.Fout, FinK = c.FinK, Mp = c.Mp, n = c.n;
   const int li = c.li, h = c.h, wave = c.wave;
@@ -500,6 +540,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
   for (int i = tid; i < 32 * 3 * FV; i += kT)  // the 32 zero records
     reinterpret_cast<float*>(smem + A.E.zpos * REC)[i] = 0.f;
   __syncthreads();
+  CG_TS(A.ts, 1);
   if (CG_DBG(A.dbg, 16)) return;
 
   // A. dBasis = dy W^T  (rows m, cols j = fin*K + k, inner f) on MFMA into LDS
@@ -560,6 +601,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
       }
     }
   }
+  CG_TS(A.ts, 2);
   // the row registers and the first dW operands are loaded after phase A,
   // whose dy tiles occupy 32 registers per lane until then
   const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[wave]);
@@ -567,11 +609,17 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
   c.g1 = vzero<typename B::V>();
   c.g2 = c.g1;
   if (DW) {
-    // rows of this wave: 16 near-equal even-sized chunks of [0, M)
-    const int q = ((M + 2 * kW - 1) / (2 * kW)) * 2;
-    c.dm0 = imin(wave * q, M);
-    c.dm1 = imin(c.dm0 + q, M);
-    c.npair = (c.dm1 - c.dm0 + 1) >> 1;
+    if (B::OB) {  // row quads wave, wave + 16, ... (dw_row)
+      const int nq = (M + 3) >> 2;
+      c.dm0 = 0;
+      c.dm1 = M;
+      c.npair = wave < nq ? 2 * ((nq - wave + kW - 1) / kW) : 0;
+    } else {  // rows of this wave: 16 near-equal even-sized chunks of [0, M)
+      const int q = ((M + 2 * kW - 1) / (2 * kW)) * 2;
+      c.dm0 = imin(wave * q, M);
+      c.dm1 = imin(c.dm0 + q, M);
+      c.npair = (c.dm1 - c.dm0 + 1) >> 1;
+    }
 #pragma unroll
     for (int e = 0; e < 16; ++e) c.dacc[e] = 0.f;
     c.dw_load(0, 0);
@@ -579,6 +627,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
     c.dw_load(2, 2 * B::NU);
   }
   __syncthreads();
+  CG_TS(A.ts, 3);
 
   // B. reverse recurrence over L~^T (+ dW MFMAs between steps)
   switch (wl) {
@@ -588,6 +637,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
 #undef CG_L
     default: break;
   }
+  CG_TS(A.ts, 4);
 
   if (DW) {
     // remaining row pairs (K small relative to M/32), then the cross-wave sum
@@ -609,6 +659,7 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
       if (j < FinK && f < Fout) A.dw_slab[(size_t(n) * FinK + j) * Fout + f] = s;
     }
   }
+  CG_TS(A.ts, 5);
 }
 
 template <typename Kern>
@@ -617,15 +668,15 @@ hipError_t allow_big_lds(Kern k) {
                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
 }
 
-template <int FV, int NT>
+template <int FV, int NT, bool OB>
 hipError_t launch_fwd_fast_t(size_t lds, int N, const FastFwdArgs& a, hipStream_t s) {
-  static hipError_t attr = allow_big_lds(&cheb_fwd_fast<FV, NT>);
+  static hipError_t attr = allow_big_lds(&cheb_fwd_fast<FV, NT, OB>);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((cheb_fwd_fast<FV, NT>), dim3(N), dim3(kT), lds, s, a);
+  hipLaunchKernelGGL((cheb_fwd_fast<FV, NT, OB>), dim3(N), dim3(kT), lds, s, a);
   return hipGetLastError();
 }
 
-template <int FV, bool DW>
+template <int FV, int DW>
 hipError_t launch_bwd_fast_t(size_t lds, int N, const FastBwdArgs& a, hipStream_t s) {
   static hipError_t attr = allow_big_lds(&cheb_bwd_fast<FV, DW>);
   if (attr != hipSuccess) return attr;

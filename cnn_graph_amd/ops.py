@@ -175,38 +175,62 @@ class ChebRunner:
     and the backward share ONE buffer of max(fwd, bwd) bytes (config D at
     N = 256: 51.5 GB instead of 68.7 GB)."""
 
-    def __init__(self, plan: ChebPlan, N: int, Fin: int, K: int, Fout: int, device):
+    def __init__(self, plan: ChebPlan, N: int, Fin: int, K: int, Fout: int, device,
+                 basis_layout: str = "rows"):
+        """basis_layout: 'rows' ([N*M, Fin*K], lib/graph_conv.py:172), 'orders'
+        ([N, Fin*K, Mb], one plane per order: the fast forward stores it during
+        the recurrence; fast path with fused dW only) or 'auto' (orders where it
+        applies).  The basis is this runner's saved tensor either way."""
         self.plan, self.N, self.Fin, self.K, self.Fout = plan, int(N), int(Fin), int(K), int(Fout)
         dev = torch.device(device)
         self.path = plan.query_path(N, Fin, K, Fout)
         fb, bb = plan.workspace_bytes(N, Fin, K, Fout)
         M = plan.M
         f32 = dict(device=dev, dtype=torch.float32)
-        self.basis = torch.empty((N * M, Fin * K), **f32)
+        if basis_layout == "auto":
+            basis_layout = "orders" if plan.basis_elems(N, Fin, K, Fout, "orders") else "rows"
+        if basis_layout == "orders":
+            if plan.basis_elems(N, Fin, K, Fout, "orders") is None:
+                raise ValueError("orders basis layout does not apply to this shape "
+                                 "(needs the fast forward and the fused-dW fast backward)")
+            self.basis = torch.empty((N, Fin * K, (M + 31) // 32 * 32), **f32)
+        elif basis_layout == "rows":
+            self.basis = torch.empty((N * M, Fin * K), **f32)
+        else:
+            raise ValueError(f"unknown basis layout {basis_layout!r}")
+        self.basis_layout = basis_layout
+        self._lay = _lib.BASIS_LAYOUTS[basis_layout]
         self.y = torch.empty((N, M, Fout), **f32)
         self.dx = torch.empty((N, M, Fin), **f32)
         self.dW = torch.empty((Fin * K, Fout), **f32)
         self.ws = torch.empty(max(fb, bb, 1), device=dev, dtype=torch.uint8)
         self.fws = self.bws = self.ws
         self.fwd_bytes, self.bwd_bytes = fb, bb
-        self._fwd = _lib.lib().cg_cheb_forward
-        self._bwd = _lib.lib().cg_cheb_backward
+        self._fwd = _lib.lib().cg_cheb_forward_layout
+        self._bwd = _lib.lib().cg_cheb_backward_layout
+
+    def basis_rows(self) -> torch.Tensor:
+        """The saved basis as [N*M, Fin*K] (a copy when the layout is 'orders')."""
+        if self.basis_layout == "rows":
+            return self.basis
+        M = self.plan.M
+        return self.basis[:, :, :M].permute(0, 2, 1).reshape(self.N * M, self.Fin * self.K)
 
     def forward(self, x: torch.Tensor, W: torch.Tensor, stream=None):
         s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
         st = self._fwd(self.plan.handle, self.N, self.Fin, self.K, self.Fout, x.data_ptr(),
-                       W.data_ptr(), self.basis.data_ptr(), self.y.data_ptr(), self.fws.data_ptr(),
-                       self.fwd_bytes, s)
-        _lib.check("cg_cheb_forward", st)
+                       W.data_ptr(), None, 0, self._lay, self.basis.data_ptr(), self.y.data_ptr(),
+                       self.fws.data_ptr(), self.fwd_bytes, s)
+        _lib.check("cg_cheb_forward_layout", st)
         return self.y
 
     def backward(self, dy: torch.Tensor, W: torch.Tensor, need_dx: bool = True, stream=None):
         s = stream if stream is not None else torch.cuda.current_stream(dy.device).cuda_stream
-        st = self._bwd(self.plan.handle, self.N, self.Fin, self.K, self.Fout, dy.data_ptr(),
-                       self.basis.data_ptr(), W.data_ptr(),
-                       self.dx.data_ptr() if need_dx else None, self.dW.data_ptr(),
+        st = self._bwd(self.plan.handle, self.N, self.Fin, self.K, self.Fout, dy.data_ptr(), None, 0,
+                       self._lay, self.basis.data_ptr(), W.data_ptr(),
+                       self.dx.data_ptr() if need_dx else None, 0, self.dW.data_ptr(), None,
                        self.bws.data_ptr(), self.bwd_bytes, s)
-        _lib.check("cg_cheb_backward", st)
+        _lib.check("cg_cheb_backward_layout", st)
         return (self.dx if need_dx else None), self.dW
 
     def backward_adam(self, dy: torch.Tensor, W: torch.Tensor, m: torch.Tensor, v: torch.Tensor,
@@ -214,19 +238,19 @@ class ChebRunner:
                       eps: float = 1e-8, grad_scale: float = 1.0, need_dx: bool = True,
                       stream=None):
         """backward + Adam on W in place, the update fused into the dW reduction
-        (cg_cheb_backward_adam; one-GPU step, lib/graph_model.py:277-298)."""
+        (cg_cheb_backward_adam_layout; one-GPU step, lib/graph_model.py:277-298)."""
         shape = (self.Fin * self.K, self.Fout)
         for name, t_ in (("W", W), ("m", m), ("v", v)):
             _check_out(name, t_, shape)   # updated in place for i < Fin*K*Fout
         if len({W.data_ptr(), m.data_ptr(), v.data_ptr(), self.dW.data_ptr()}) != 4:
             raise ValueError("backward_adam: W, m, v and dW must be distinct buffers")
         s = stream if stream is not None else torch.cuda.current_stream(dy.device).cuda_stream
-        st = _lib.lib().cg_cheb_backward_adam(
-            self.plan.handle, self.N, self.Fin, self.K, self.Fout, dy.data_ptr(),
+        st = _lib.lib().cg_cheb_backward_adam_layout(
+            self.plan.handle, self.N, self.Fin, self.K, self.Fout, self._lay, dy.data_ptr(),
             self.basis.data_ptr(), W.data_ptr(), self.dx.data_ptr() if need_dx else None,
             self.dW.data_ptr(), m.data_ptr(), v.data_ptr(), lr, beta1, beta2, eps, step,
             grad_scale, self.bws.data_ptr(), self.bwd_bytes, s)
-        _lib.check("cg_cheb_backward_adam", st)
+        _lib.check("cg_cheb_backward_adam_layout", st)
         return (self.dx if need_dx else None), self.dW
 
 

@@ -98,6 +98,18 @@ class ChebPlan:
         """(forward, backward) device workspace bytes for this shape."""
         return self._shape_info(N, Fin, K, Fout)[1:]
 
+    def basis_elems(self, N, Fin, K, Fout, layout: str = "rows"):
+        """Floats of the basis buffer in ``layout`` ('rows' [N*M, Fin*K] or 'orders'
+        [N, Fin*K, Mb]), or None where the layout does not apply to this shape
+        (cg_cheb_basis_elems)."""
+        n = ctypes.c_int64()
+        st = self._lib.cg_cheb_basis_elems(self._h, N, Fin, K, Fout, _lib.BASIS_LAYOUTS[layout],
+                                           ctypes.byref(n))
+        if st == 3:  # CG_ERR_UNSUPPORTED
+            return None
+        _lib.check("cg_cheb_basis_elems", st)
+        return int(n.value)
+
     def close(self):
         self._ws = {}
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -141,6 +141,34 @@ int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_
                         const float* dy, const float* y, int32_t act, const float* basis,
                         const float* W, float* dx, int32_t dx_accumulate, float* dW, float* dz,
                         void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Basis layouts.  The basis is the forward's saved tensor (the x of
+ * lib/graph_conv.py:172 that TF keeps for the matmul gradient at :175); its
+ * layout is the caller's choice per call pair:
+ *   CG_BASIS_ROWS    [N*M][Fin*K]   (:172; every path; the default of the calls above)
+ *   CG_BASIS_ORDERS  [N][Fin*K][Mb] (Mb = M rounded up to 32; rows >= M hold 0):
+ *                    one contiguous plane per Chebyshev order, so the fast forward
+ *                    stores each order pair while the recurrence runs instead of
+ *                    after it.  Only for Fin <= 2 where the fast resident forward
+ *                    AND the fused-dW fast backward apply (else CG_ERR_UNSUPPORTED),
+ *                    and the backward must compute dx with dW.
+ * Same values either way (bit-exact basis, y and dx; dW sums its per-wave row
+ * chunks in another grouping, so it agrees to fp32 rounding).
+ * cg_cheb_basis_elems: floats the basis buffer of that layout holds, or
+ * CG_ERR_UNSUPPORTED where the layout does not apply.
+ * ------------------------------------------------------------------------- */
+enum { CG_BASIS_ROWS = 0, CG_BASIS_ORDERS = 1 };
+int cg_cheb_basis_elems(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                        int32_t layout, int64_t* elems);
+int cg_cheb_forward_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                           const float* x, const float* W, const float* residual, int32_t act,
+                           int32_t layout, float* basis, float* y, void* workspace,
+                           size_t ws_bytes, void* stream);
+int cg_cheb_backward_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                            const float* dy, const float* y, int32_t act, int32_t layout,
+                            const float* basis, const float* W, float* dx, int32_t dx_accumulate,
+                            float* dW, float* dz, void* workspace, size_t ws_bytes, void* stream);
 /* MSE loss of lib/graph_model.py:255, tf.reduce_mean(tf.square(labels - logits)),
  * over n elements: *loss (device scalar) and dpred = 2 (pred - labels) / n
  * (NULL to skip).  Fixed-order reduction (bitwise reproducible). */
@@ -312,6 +340,12 @@ int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int3
                           float* m, float* v, float lr, float beta1, float beta2, float eps,
                           int32_t step, float grad_scale, void* workspace, size_t ws_bytes,
                           void* stream);
+/* The same with the basis in a chosen layout (CG_BASIS_*, see cg_cheb_basis_elems). */
+int cg_cheb_backward_adam_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                                 int32_t layout, const float* dy, const float* basis, float* W,
+                                 float* dx, float* dW, float* m, float* v, float lr, float beta1,
+                                 float beta2, float eps, int32_t step, float grad_scale,
+                                 void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Graph coarsening (host code; no device work).

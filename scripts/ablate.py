@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--path", default="resident")
+    ap.add_argument("--layout", default="rows", choices=["rows", "orders"],
+                    help="basis layout of the default-variant runner")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     L, fake = bench.load_config_b()
@@ -47,7 +49,9 @@ def main():
     W = torch.randn((K, Fout), device=dev) * 0.1
     dy = torch.randn((N, M, Fout), device=dev)
     runners = {v: ops.ChebRunner(ChebPlan.from_laplacian(L, 2, 0, path=args.path, variant=v),
-                                 N, Fin, K, Fout, dev) for v in ("auto", "classic", "unfused_dw")}
+                                 N, Fin, K, Fout, dev,
+                                 basis_layout=args.layout if v == "auto" else "rows")
+               for v in ("auto", "classic", "unfused_dw")}
     r = runners["auto"]
     h = _lib.lib()
     h.cg_debug_set_flags.argtypes = [ctypes_int()]
@@ -87,7 +91,7 @@ def main():
     sweep = {}
     for Kx in (2, 7, 13, 25):
         Wx = torch.randn((Kx, Fout), device=dev) * 0.1
-        rx = ops.ChebRunner(plan, N, Fin, Kx, Fout, dev)
+        rx = ops.ChebRunner(plan, N, Fin, Kx, Fout, dev, basis_layout=args.layout)
         for name, f in (("fwd_full", 0), ("fwd_only_spmm", FWD["only_spmm"][0]), ("bwd_full", 0),
                         ("bwd_no_dw", 1 << 22)):
             vals = []
@@ -110,7 +114,7 @@ def main():
                 vals.append(e0.elapsed_time(e1) / args.reps * 1e3)
             sweep[f"K{Kx}:{name}"] = round(float(np.median(vals)), 2)
     h.cg_debug_set_flags(0)
-    print(json.dumps({"batch": N, "path": args.path, "us_median": out, "k_sweep": sweep}, indent=1))
+    print(json.dumps({"batch": N, "path": args.path, "layout": args.layout, "us_median": out, "k_sweep": sweep}, indent=1))
 
 
 def ctypes_int():

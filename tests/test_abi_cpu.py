@@ -108,3 +108,21 @@ def test_stack_merge_and_loss_ema_entry_points_validate(built_lib):
     assert h.cg_stack_merge_backward(2, 10, 2, p, q, r, p, None, None) == _lib.CG_ERR_ARG
     assert h.cg_mse_loss_ema(p, q, 10, r, None, None, 0.9, None, 0, None) == _lib.CG_ERR_ARG
     assert h.cg_mse_loss_ema(p, q, 10, r, None, r, 1.5, None, 0, None) == _lib.CG_ERR_ARG
+
+
+def test_basis_layout_entry_points_validate(built_lib):
+    """Orders-layout entry points reject a null plan / unknown layout before any
+    device work (no GPU needed)."""
+    h = _lib.lib()
+    n = ctypes.c_int64()
+    assert h.cg_cheb_basis_elems(None, 1, 1, 2, 1, _lib.CG_BASIS_ORDERS, ctypes.byref(n)) == _lib.CG_ERR_ARG
+    assert h.cg_cheb_forward_layout(None, 1, 1, 2, 1, None, None, None, 0, _lib.CG_BASIS_ORDERS,
+                                    None, None, None, 0, None) == _lib.CG_ERR_ARG
+    assert h.cg_cheb_backward_layout(None, 1, 1, 2, 1, None, None, 0, _lib.CG_BASIS_ORDERS, None,
+                                     None, None, 0, None, None, None, 0, None) == _lib.CG_ERR_ARG
+    assert h.cg_cheb_backward_adam_layout(None, 1, 1, 2, 1, _lib.CG_BASIS_ORDERS, None, None, None,
+                                          None, None, None, None, 1e-3, 0.9, 0.999, 1e-8, 1, 1.0,
+                                          None, 0, None) == _lib.CG_ERR_ARG
+    assert h.cg_cheb_backward_layout(None, 1, 1, 2, 1, None, None, 7, _lib.CG_BASIS_ORDERS, None,
+                                     None, None, 0, None, None, None, 0, None) == _lib.CG_ERR_ARG
+    assert "activation" in h.cg_last_error().decode()

@@ -1,0 +1,147 @@
+"""Orders basis layout (CG_BASIS_ORDERS, [N][Fin*K][Mb]): the fast forward
+stores each Chebyshev order pair during the recurrence and the fused-dW fast
+backward reads the planes back.  Bar: basis (re-laid to rows), y and dx
+BITWISE equal to the rows layout (lib/graph_conv.py:172) and the basis bitwise
+equal to the reference-generated golden basis; padding rows zero; dW (which
+sums its per-wave row chunks in another grouping) within 1e-6 normwise of the
+rows-layout dW and 1e-5 of the golden/oracle dW; Adam on top agrees."""
+import numpy as np
+import pytest
+import scipy.sparse
+
+from conftest import case, load_golden
+from oracle import cheb_oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(built_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_graph_amd import _lib
+    _lib.lib()
+    return torch.device("cuda", 0)
+
+
+def _plan(c):
+    from cnn_graph_amd.plan import ChebPlan
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    return ChebPlan(Lt, device=0, path="resident")
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+
+
+def _pair(plan, N, Fin, K, Fout, dev, x, W, dy):
+    from cnn_graph_amd import ops
+    rr = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
+    ro = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="orders")
+    assert ro.basis_layout == "orders"
+    for r in (rr, ro):
+        r.forward(x, W)
+        r.backward(dy, W)
+    torch.cuda.synchronize()
+    return rr, ro
+
+
+def _check_pair(rr, ro, M):
+    assert torch.equal(ro.basis_rows(), rr.basis), "orders basis differs from the rows basis"
+    assert int(torch.count_nonzero(ro.basis[:, :, M:])) == 0, "padding rows not zero"
+    assert torch.equal(ro.y, rr.y)
+    assert torch.equal(ro.dx, rr.dx)
+    assert O.normwise_err(ro.dW.cpu().double().numpy(), rr.dW.cpu().double().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["golden_B.npz", "golden_E.npz"])
+def test_orders_layout_golden(dev, name):
+    c = case(load_golden(name))
+    M, N, Fin, K, Fout = c["M"], c["N"], c["Fin"], c["K"], c["Fout"]
+    plan = _plan(c)
+    Mb = (M + 31) // 32 * 32
+    assert plan.basis_elems(N, Fin, K, Fout, "orders") == N * Fin * K * Mb
+    assert plan.basis_elems(N, Fin, K, Fout, "rows") == N * M * Fin * K
+    rr, ro = _pair(plan, N, Fin, K, Fout, dev, _t(c["x"], dev), _t(c["W"], dev), _t(c["dy"], dev))
+    _check_pair(rr, ro, M)
+    assert np.array_equal(ro.basis_rows().cpu().numpy(), c["basis"].astype(np.float32))
+    assert O.normwise_err(ro.y.cpu().double().numpy(), c["y_ref"]) < 1e-5
+    assert O.normwise_err(ro.dx.cpu().double().numpy(), c["dx_ref"]) < 1e-5
+    assert O.normwise_err(ro.dW.cpu().double().numpy(), c["dW_ref"]) < 1e-5
+
+
+@pytest.mark.parametrize("N,Fin,K", [(256, 1, 25), (96, 2, 8), (64, 2, 3), (40, 1, 2), (33, 1, 1)])
+def test_orders_layout_config_b_shapes(dev, N, Fin, K):
+    """Config B's graph at the bench batch (N = 256) and at other Fin/K/N,
+    including K = 1 (no recurrence) and K = 2 (one half-empty pair)."""
+    c = case(load_golden("golden_B.npz"))
+    M, Fout = c["M"], 32
+    plan = _plan(c)
+    g = torch.Generator().manual_seed(1000 + N + Fin + K)
+    x = torch.rand((N, M, Fin), generator=g).to(dev)
+    W = (torch.randn((Fin * K, Fout), generator=g) * 0.1).to(dev)
+    dy = torch.randn((N, M, Fout), generator=g).to(dev)
+    rr, ro = _pair(plan, N, Fin, K, Fout, dev, x, W, dy)
+    _check_pair(rr, ro, M)
+    # against the oracle (basis bit-exact, dW / dx to 1e-5) where it is quick
+    if N <= 64:
+        rp, ci, va = c["Lt_rowptr"], c["Lt_col"], c["Lt_val"]
+        xs, Ws, dys = (t.cpu().numpy() for t in (x, W, dy))
+        basis, _ = O.cheb_forward(xs, rp, ci, va, Ws, K)
+        assert np.array_equal(ro.basis_rows().cpu().numpy(), basis)
+        dx64, dW64 = O.cheb_backward(dys, basis, Ws, rp, ci, va, N, M, Fin, K)
+        assert O.normwise_err(ro.dW.cpu().double().numpy(), dW64) < 1e-5
+        assert O.normwise_err(ro.dx.cpu().double().numpy(), dx64) < 1e-5
+
+
+def test_orders_layout_adam(dev):
+    c = case(load_golden("golden_B.npz"))
+    M, N, Fin, K, Fout = c["M"], c["N"], c["Fin"], c["K"], c["Fout"]
+    from cnn_graph_amd import ops
+    plan = _plan(c)
+    x, dy, W0 = _t(c["x"], dev), _t(c["dy"], dev), _t(c["W"], dev)
+    rr = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
+    ro = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="orders")
+    Wr, Wo = W0.clone(), W0.clone()
+    mr, vr, mo, vo = (torch.zeros_like(W0) for _ in range(4))
+    for step in (1, 2, 3):
+        rr.forward(x, Wr)
+        ro.forward(x, Wo)
+        rr.backward_adam(dy, Wr, mr, vr, step)
+        ro.backward_adam(dy, Wo, mo, vo, step)
+        torch.cuda.synchronize()
+        if step == 1:  # later steps start from W that differ by dW's rounding
+            assert torch.equal(ro.dx, rr.dx), "dx differs at equal W"
+        else:
+            assert O.normwise_err(ro.dx.cpu().double().numpy(), rr.dx.cpu().double().numpy()) < 1e-5
+        assert O.normwise_err(Wo.cpu().double().numpy(), Wr.cpu().double().numpy()) < 1e-6
+
+
+def test_orders_layout_unsupported(dev):
+    from cnn_graph_amd import _lib, ops
+    c = case(load_golden("golden_B.npz"))
+    M = c["M"]
+    plan = _plan(c)
+    # Fout = 64: no fused dW in the fast backward -> rows only
+    assert plan.basis_elems(8, 1, 25, 64, "orders") is None
+    with pytest.raises(ValueError):
+        ops.ChebRunner(plan, 8, 1, 25, 64, dev, basis_layout="orders")
+    assert ops.ChebRunner(plan, 8, 1, 25, 64, dev, basis_layout="auto").basis_layout == "rows"
+    assert ops.ChebRunner(plan, 8, 1, 25, 32, dev, basis_layout="auto").basis_layout == "orders"
+    # config A's graph has a 21-nonzero row: classic resident kernels, rows only
+    a = case(load_golden("golden_A.npz"))
+    assert _plan(a).basis_elems(a["N"], 1, a["K"], a["Fout"], "orders") is None
+    # the streaming path never takes it
+    from cnn_graph_amd.plan import ChebPlan
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    assert ChebPlan(Lt, device=0, path="stream").basis_elems(8, 1, 25, 32, "orders") is None
+    # dW is fused into the dx pass: dW without dx is refused
+    ro = ops.ChebRunner(plan, 8, 1, 25, 32, dev, basis_layout="orders")
+    x = torch.rand((8, M, 1), device=dev)
+    W = torch.randn((25, 32), device=dev)
+    ro.forward(x, W)
+    with pytest.raises(_lib.CGError):
+        ro.backward(torch.randn((8, M, 32), device=dev), W, need_dx=False)
+
