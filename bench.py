@@ -199,8 +199,8 @@ def main():
     ap.add_argument("--global-batch", type=int, default=None,
                     help="fixed whole-job batch sharded over the ranks (strong scaling)")
     ap.add_argument("--path", default="auto", choices=["auto", "resident", "stream"])
-    ap.add_argument("--basis-layout", default="auto", choices=["auto", "rows", "orders"],
-                    help="saved-basis layout (orders where the fast kernels apply)")
+    ap.add_argument("--basis-layout", default="rows", choices=["rows", "orders"],
+                    help="saved-basis layout (orders: fast kernels, Fin <= 2 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "torch"],
@@ -246,8 +246,8 @@ def main():
     m_adam = torch.zeros_like(W)
     v_adam = torch.zeros_like(W)
 
-    # the orders basis layout where the fast kernels apply (config B): the
-    # forward stores the basis during its recurrence (cg_cheb_basis_elems)
+    # basis layout: rows by default (the orders layout's faster forward is
+    # outweighed by its slower fused-dW backward on config B: DESIGN.md §5)
     runner = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=args.basis_layout)
     stream = torch.cuda.current_stream(dev).cuda_stream
     adam = _lib.lib().cg_adam_update

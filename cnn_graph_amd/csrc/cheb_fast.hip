@@ -21,7 +21,7 @@ FastGeom fast_geometry(int M, int P, int max_row_nnz, int max_row_nnzT, int Fin,
   g.nt = (Fout + 31) / 32;
   g.fwd_lds_ob = ring + align16(FinK * Fout * 4);  // orders layout: no basis staging
   g.fwd_lds = g.fwd_lds_ob + size_t(M) * FinK * 4;
-  g.dw_fused = FinK <= 32 && Fout <= 32;
+  g.dw_fused = FinK <= 32 && Fout <= 32 && Fout % 8 == 0;  // (the phase-A tile loads of cheb_bwd_fast)
   const size_t d_bytes = FinK * size_t(lds_vertex_stride(M)) * 4;
   g.dscratch = g.dw_fused ? std::max<size_t>(d_bytes, 16 * 32 * 32 * 4) : d_bytes;
   g.bwd_lds = ring + align16(g.dscratch) + FinK * (Fout + 1) * 4;

@@ -110,6 +110,14 @@ template <>
 __device__ __forceinline__ float2 vzero<float2>() { return make_float2(0.f, 0.f); }
 template <>
 __device__ __forceinline__ float4 vzero<float4>() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+// order-only dependence: x is "rewritten" by an empty asm that reads a
+__device__ __forceinline__ void pin(float& a, float& x) { asm volatile("" : "+v"(a), "+v"(x)); }
+__device__ __forceinline__ void pin(float2& a, float& x) {
+  asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(x));
+}
+__device__ __forceinline__ void pin(float4& a, float& x) {
+  asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(x));
+}
 __device__ __forceinline__ float comp(float v, int) { return v; }
 __device__ __forceinline__ float comp(float2 v, int i) { return i == 0 ? v.x : v.y; }
 __device__ __forceinline__ float comp(float4 v, int i) {
@@ -131,36 +139,47 @@ struct Row {
   int ca[kFastWidth];  // byte offsets of the gathered records (zero record = padding)
   float v[kFastWidth];
 
-  template <int FV>
-  __device__ __forceinline__ void load(const FastImage& E, int tid, int wl) {
+  // NL: slots loaded -- kFastWidth, or the wave's row length when the caller
+  // is already specialised on it (no per-slot branches: loading the first wl
+  // slots under runtime conditions was measured SLOWER, the branches
+  // serialise the loads; a compile-time count does not branch at all)
+  template <int FV, int NL = kFastWidth>
+  __device__ __forceinline__ void load(const FastImage& E, int tid) {
     constexpr int REC = 12 * FV;
     row = E.row[tid];
     rb = E.rpos[tid] * REC;
     rb1 = E.rpos1[tid] * REC;
     rr = E.rposr[tid] * REC;
-    (void)wl;  // loading only the first wl slots was measured SLOWER (per-slot
-               // branches serialise the loads): load all 16 unconditionally
 #pragma unroll
-    for (int j2 = 0; j2 < kFastWidth / 2; ++j2) {
+    for (int j2 = 0; j2 < (NL + 1) / 2; ++j2) {
       const uint32_t pk = uint32_t(E.cpos[j2 * kT + tid]);
       ca[2 * j2] = int(pk & 0xffffu) * REC;
       ca[2 * j2 + 1] = int(pk >> 16) * REC;
     }
 #pragma unroll
-    for (int j = 0; j < kFastWidth; ++j) v[j] = E.val[j * kT + tid];
+    for (int j = 0; j < NL; ++j) v[j] = E.val[j * kT + tid];
   }
 
-  // sum_{j < L, CSR order} v_j * T[c_j][SLOT]  (sequential, one rounding each)
+  // the L gathers T[c_j][SLOT] of a step, issued together
   template <int FV, int L, int SLOT>
-  __device__ __forceinline__ typename VecT<FV>::type dot(const char* ring) const {
-    typedef typename VecT<FV>::type V;
-    V g[L > 0 ? L : 1];
+  __device__ __forceinline__ void gather(const char* ring, typename VecT<FV>::type* g) const {
 #pragma unroll
     for (int j = 0; j < L; ++j) g[j] = lds_v<FV>(ring + ca[j] + SLOT * 4 * FV);
+  }
+  // sum_{j < L, CSR order} v_j * g_j  (sequential, one rounding each)
+  template <int FV, int L>
+  __device__ __forceinline__ typename VecT<FV>::type reduce(const typename VecT<FV>::type* g) const {
+    typedef typename VecT<FV>::type V;
     V a = vzero<V>();
 #pragma unroll
     for (int j = 0; j < L; ++j) a = madd(a, v[j], g[j]);
     return a;
+  }
+  template <int FV, int L, int SLOT>
+  __device__ __forceinline__ typename VecT<FV>::type dot(const char* ring) const {
+    typename VecT<FV>::type g[L > 0 ? L : 1];
+    gather<FV, L, SLOT>(ring, g);
+    return reduce<FV, L>(g);
   }
 };
 
@@ -263,6 +282,48 @@ struct Fwd {
   }
 
   template <int L>
+  __device__ __forceinline__ void go() {
+    constexpr int REC_ = REC;
+    const int tid = threadIdx.x;
+    const int n = blockIdx.x;
+    r.template load<FV, L>(A.E, tid);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int tile = imin(wave + t * kW, ntiles - 1);
+      mb[t] = A.E.mpos[tile * 32 + li] * REC_;
+    }
+    char* smem = ring;
+    for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = A.W ? A.W[i] : 0.f;
+    // T_0 = x into ring slot 0 ([pos][0][fin]); zero record kept at 0
+    const float* xn = A.x + size_t(n) * M * FV;
+    for (int i = tid; i < M * FV; i += kT) {
+      const int m = i / FV, fin = i - m * FV;
+      const float xv = xn[i];
+      reinterpret_cast<float*>(smem + A.E.pos0[m] * REC_)[fin] = xv;
+      reinterpret_cast<float*>(smem + A.E.pos1[m] * REC_)[fin] = xv;
+    }
+    for (int i = tid; i < 32 * 3 * FV; i += kT)  // the 32 zero records
+      reinterpret_cast<float*>(smem + A.E.zpos * REC_)[i] = 0.f;
+    // T_0 of the own row for the register-held T_{k-2}
+    t1 = vzero<V>();
+    if (r.row >= 0) {
+#pragma unroll
+      for (int fin = 0; fin < FV; ++fin) setc(t1, fin, xn[r.row * FV + fin]);
+    }
+    t2 = t1;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][q][e] = 0.f;
+    __syncthreads();
+    CG_TS(A.ts, 1);
+    if (CG_DBG(A.dbg, 16)) return;
+    run<L>();
+  }
+
+  template <int L>
   __device__ __forceinline__ void run() {
     for (int k = 1; k < K; k += 6) {  // k = 1 (mod 6): slots cur/prv/prv2 = 1/0/2
       step<L, 1, 0, 2>(k);
@@ -281,55 +342,23 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef Fwd<FV, NT, OB> F;
-  constexpr int REC = F::REC;
   const int tid = threadIdx.x;
   const int n = blockIdx.x;
   CG_TS(A.ts, 0);
   F c(A, smem, tid);
   const int M = c.M, Fout = c.Fout, FinK = c.FinK;
 
+  // the whole prologue is specialised on the wave's row length, so each
+  // thread loads exactly the L gather slots its run<L> uses
   const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[c.wave]);
-  c.r.template load<FV>(A.E, tid, wl);
-#pragma unroll
-  for (int t = 0; t < F::MT; ++t) {
-    const int tile = imin(c.wave + t * kW, c.ntiles - 1);
-    c.mb[t] = A.E.mpos[tile * 32 + c.li] * REC;
-  }
-  for (int i = tid; i < FinK * Fout; i += kT) c.s_W[i] = A.W ? A.W[i] : 0.f;
-  // T_0 = x into ring slot 0 ([pos][0][fin]); zero record kept at 0
-  const float* xn = A.x + size_t(n) * M * FV;
-  for (int i = tid; i < M * FV; i += kT) {
-    const int m = i / FV, fin = i - m * FV;
-    const float xv = xn[i];
-    reinterpret_cast<float*>(smem + A.E.pos0[m] * REC)[fin] = xv;
-    reinterpret_cast<float*>(smem + A.E.pos1[m] * REC)[fin] = xv;
-  }
-  for (int i = tid; i < 32 * 3 * FV; i += kT)  // the 32 zero records
-    reinterpret_cast<float*>(smem + A.E.zpos * REC)[i] = 0.f;
-  // T_0 of the own row for the register-held T_{k-2}
-  c.t1 = vzero<typename F::V>();
-  if (c.r.row >= 0) {
-#pragma unroll
-    for (int fin = 0; fin < FV; ++fin) setc(c.t1, fin, xn[c.r.row * FV + fin]);
-  }
-  c.t2 = c.t1;
-#pragma unroll
-  for (int t = 0; t < F::MT; ++t)
-#pragma unroll
-    for (int q = 0; q < NT; ++q)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) c.acc[t][q][e] = 0.f;
-  __syncthreads();
-  CG_TS(A.ts, 1);
-  if (CG_DBG(A.dbg, 16)) return;
-
   switch (wl) {
-#define CG_L(L_) case L_: c.template run<L_>(); break;
+#define CG_L(L_) case L_: c.template go<L_>(); break;
     CG_L(0) CG_L(1) CG_L(2) CG_L(3) CG_L(4) CG_L(5) CG_L(6) CG_L(7) CG_L(8)
     CG_L(9) CG_L(10) CG_L(11) CG_L(12) CG_L(13) CG_L(14) CG_L(15) CG_L(16)
 #undef CG_L
     default: break;  // unreachable: the host only selects this kernel for rows <= 16
   }
+  if (CG_DBG(A.dbg, 16)) return;
   CG_TS(A.ts, 2);
 
   // y first: its stores leave from registers while the other waves finish
@@ -385,6 +414,7 @@ struct Bwd {
   typedef typename VecT<FV>::type V;
   static constexpr int REC = 12 * FV;
   static constexpr int NU = 2;  // dW MFMAs per recurrence step
+  static constexpr int PF = 6;  // dW operand buffers: loads run PF steps ahead
   static constexpr bool OB = DW == 2;
   static_assert(NU == 2, "the orders-layout dW loads one row quad per step");
 
@@ -397,7 +427,7 @@ struct Bwd {
   int dm0, dm1, npair, nexti;
   V g1, g2;  // G_{k+1}, G_{k+2} of the own row
   f32x16 dacc;
-  float da[3][NU], db[3][NU];
+  float da[PF][NU], db[PF][NU];
 
   __device__ __forceinline__ Bwd(const FastBwdArgs& a, char* smem, int tid) : A(a) {
     K = a.K;
@@ -447,29 +477,44 @@ struct Bwd {
       db[buf][u] = dyn[size_t(m) * Fout + fc];
     }
   }
+  // MFMA u of the NU held in buffer buf (the u-th row pair from i0).  With
+  // `after` given, the MFMA is pinned behind the computation of *after: its
+  // operand passes through an empty asm that also consumes *after (the
+  // compiler otherwise hoists it next to MFMA 0, ahead of the reduction)
+  template <typename T = float>
+  __device__ __forceinline__ void dw_mfma1(int buf, int i0, int u, T* after = nullptr) {
+    const int i = i0 + u;
+    if (i < npair) {
+      const bool rv = dw_row(i) < dm1;
+      float x = da[buf][u];
+      if (after) pin(*after, x);
+      dacc = mfma32((rv && li < FinK) ? x : 0.f, (rv && li < Fout) ? db[buf][u] : 0.f, dacc);
+    }
+  }
   __device__ __forceinline__ void dw_mfma(int buf, int i0) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int i = i0 + u;
-      if (i < npair) {
-        const bool rv = dw_row(i) < dm1;
-        dacc = mfma32((rv && li < FinK) ? da[buf][u] : 0.f, (rv && li < Fout) ? db[buf][u] : 0.f,
-                      dacc);
-      }
-    }
+    for (int u = 0; u < NU; ++u) dw_mfma1(buf, i0, u);
   }
 
   template <int L, int CUR, int NX1, int NX2, int BUF>
   __device__ __forceinline__ void step(int i) {
 #pragma clang fp contract(off)
     const int k = K - 1 - i;
-    if (DW) {  // consume the operands loaded three steps ago, refill for step i + 3
-      dw_mfma(BUF, i * NU);
-      dw_load(BUF, (i + 3) * NU);
-    }
+    // The step's gathers go out first, then the step's two dW MFMAs
+    // (operands loaded PF steps ago) one on each side of the reduction: the
+    // matrix pipe works while the wave waits for LDS, and a wave never stalls
+    // in order behind its own dependent MFMA.  (Both MFMAs ahead of the
+    // gathers queued the SIMD's four waves behind 8 MFMAs -- 512 cycles --
+    // every step: measured +4.5 us over the recurrence.)
+    V gth[L > 0 ? L : 1];
+    if (i >= 1) r.template gather<FV, L, NX1>(ring, gth);
+    // (ablation build: bit 64 skips the dW MFMAs, bit 128 the dW loads)
+    if (DW && !CG_DBG(A.dbg, 64)) dw_mfma1(BUF, i * NU, 0);
     const float c = (k >= 1) ? 2.f : 1.f;
     V a = vzero<V>();
-    if (i >= 1) a = r.template dot<FV, L, NX1>(ring);
+    if (i >= 1) a = r.template reduce<FV, L>(gth);
+    if (DW && !CG_DBG(A.dbg, 64)) dw_mfma1(BUF, i * NU, 1, &a);
+    if (DW && !CG_DBG(A.dbg, 128)) dw_load(BUF, (i + PF) * NU);  // refill for step i + PF
     // G_{k+2} of the own row: kept in registers (this thread wrote it two
     // steps ago); debug bit 32 re-reads it from the ring (A/B switch)
     const V p = CG_DBG(A.dbg, 32) ? lds_v<FV>(ring + r.rr + NX2 * 4 * FV) : g2;
@@ -497,11 +542,42 @@ struct Bwd {
   }
 
   template <int L>
+  __device__ __forceinline__ void go() {
+    r.template load<FV, L>(A.E, threadIdx.x);
+    g1 = vzero<V>();
+    g2 = g1;
+    if (DW) {
+      if (OB) {  // row quads wave, wave + 16, ... (dw_row)
+        const int nq = (M + 3) >> 2;
+        dm0 = 0;
+        dm1 = M;
+        npair = wave < nq ? 2 * ((nq - wave + kW - 1) / kW) : 0;
+      } else {  // rows of this wave: 16 near-equal even-sized chunks of [0, M)
+        const int q = ((M + 2 * kW - 1) / (2 * kW)) * 2;
+        dm0 = imin(wave * q, M);
+        dm1 = imin(dm0 + q, M);
+        npair = (dm1 - dm0 + 1) >> 1;
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dacc[e] = 0.f;
+#pragma unroll
+      for (int b = 0; b < PF; ++b) dw_load(b, b * NU);
+    }
+    __syncthreads();
+    CG_TS(A.ts, 3);
+    run<L>();
+  }
+
+  template <int L>
   __device__ __forceinline__ void run() {
-    for (int i = 0; i < K; i += 3) {
+    static_assert(PF == 6, "the loop below cycles the ring (3) and the dW buffers (6)");
+    for (int i = 0; i < K; i += 6) {
       step<L, 0, 2, 1, 0>(i);
       if (i + 1 < K) step<L, 1, 0, 2, 1>(i + 1);
       if (i + 2 < K) step<L, 2, 1, 0, 2>(i + 2);
+      if (i + 3 < K) step<L, 0, 2, 1, 3>(i + 3);
+      if (i + 4 < K) step<L, 1, 0, 2, 4>(i + 4);
+      if (i + 5 < K) step<L, 2, 1, 0, 5>(i + 5);
     }
   }
 };
@@ -523,9 +599,16 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
   const float* dyn = A.dy + size_t(n) * M * Fout;
   const int mtiles = (M + 31) >> 5, jtiles = (FinK + 31) >> 5;
   const int ns = (Fout + 1) >> 1;  // lane half h owns f in [h*ns, h*ns + ns)
+  // W first: its LDS copy (needed before the barrier) then waits only for
+  // this load, not for the dy tiles queued behind it (vmcnt is in order)
+  const int nW = FinK * Fout;
+  const float wv = tid < nW ? A.W[tid] : 0.f;
   // Fast Phase-A operand path (config B/E shapes): each wave's <= 2 dy tiles
-  // are loaded as float4 at kernel entry, overlapping the register prologue.
-  const bool fastA = mtiles <= 2 * kW && jtiles == 1 && Fout <= 32 && (Fout & 7) == 0;
+  // are loaded as float4 at kernel entry; tile 0's MFMAs start while tile 1
+  // is still in flight.  (Always taken by the fused-dW variants: the host
+  // requires FinK <= 32, Fout <= 32, Fout % 8 == 0 for them, so the loads are
+  // unconditional and the waits below count them exactly.)
+  const bool fastA = DW != 0 || (mtiles <= 2 * kW && jtiles == 1 && Fout <= 32 && (Fout & 7) == 0);
   float4 av[2][4];
   if (fastA) {
 #pragma unroll
@@ -536,7 +619,8 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
       for (int q = 0; q < 4; ++q) av[t][q] = rowp[imin(q, (ns >> 2) - 1)];
     }
   }
-  for (int i = tid; i < FinK * Fout; i += kT) s_W[(i / Fout) * ws + (i % Fout)] = A.W[i];
+  if (tid < nW) s_W[(tid / Fout) * ws + (tid % Fout)] = wv;
+  for (int i = tid + kT; i < nW; i += kT) s_W[(i / Fout) * ws + (i % Fout)] = A.W[i];
   for (int i = tid; i < 32 * 3 * FV; i += kT)  // the 32 zero records
     reinterpret_cast<float*>(smem + A.E.zpos * REC)[i] = 0.f;
   __syncthreads();
@@ -602,36 +686,13 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
     }
   }
   CG_TS(A.ts, 2);
-  // the row registers and the first dW operands are loaded after phase A,
-  // whose dy tiles occupy 32 registers per lane until then
+  // B. reverse recurrence over L~^T (+ dW MFMAs between steps); the row
+  // registers (exactly the wave's row length of them) and the first dW
+  // operands are loaded after phase A, whose dy tiles occupy 32 registers
+  // per lane until then
   const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[wave]);
-  c.r.template load<FV>(A.E, tid, wl);
-  c.g1 = vzero<typename B::V>();
-  c.g2 = c.g1;
-  if (DW) {
-    if (B::OB) {  // row quads wave, wave + 16, ... (dw_row)
-      const int nq = (M + 3) >> 2;
-      c.dm0 = 0;
-      c.dm1 = M;
-      c.npair = wave < nq ? 2 * ((nq - wave + kW - 1) / kW) : 0;
-    } else {  // rows of this wave: 16 near-equal even-sized chunks of [0, M)
-      const int q = ((M + 2 * kW - 1) / (2 * kW)) * 2;
-      c.dm0 = imin(wave * q, M);
-      c.dm1 = imin(c.dm0 + q, M);
-      c.npair = (c.dm1 - c.dm0 + 1) >> 1;
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) c.dacc[e] = 0.f;
-    c.dw_load(0, 0);
-    c.dw_load(1, B::NU);
-    c.dw_load(2, 2 * B::NU);
-  }
-  __syncthreads();
-  CG_TS(A.ts, 3);
-
-  // B. reverse recurrence over L~^T (+ dW MFMAs between steps)
   switch (wl) {
-#define CG_L(L_) case L_: c.template run<L_>(); break;
+#define CG_L(L_) case L_: c.template go<L_>(); break;
     CG_L(0) CG_L(1) CG_L(2) CG_L(3) CG_L(4) CG_L(5) CG_L(6) CG_L(7) CG_L(8)
     CG_L(9) CG_L(10) CG_L(11) CG_L(12) CG_L(13) CG_L(14) CG_L(15) CG_L(16)
 #undef CG_L

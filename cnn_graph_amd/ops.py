@@ -177,18 +177,18 @@ class ChebRunner:
 
     def __init__(self, plan: ChebPlan, N: int, Fin: int, K: int, Fout: int, device,
                  basis_layout: str = "rows"):
-        """basis_layout: 'rows' ([N*M, Fin*K], lib/graph_conv.py:172), 'orders'
+        """basis_layout: 'rows' ([N*M, Fin*K], lib/graph_conv.py:172) or 'orders'
         ([N, Fin*K, Mb], one plane per order: the fast forward stores it during
-        the recurrence; fast path with fused dW only) or 'auto' (orders where it
-        applies).  The basis is this runner's saved tensor either way."""
+        the recurrence; Fin <= 2 fast path with fused dW only).  The basis is
+        this runner's saved tensor either way.  On config B the orders layout
+        makes the forward ~1.3 us faster and the backward ~1.9 us slower
+        (profiles/r02_orders), so 'rows' stays the default."""
         self.plan, self.N, self.Fin, self.K, self.Fout = plan, int(N), int(Fin), int(K), int(Fout)
         dev = torch.device(device)
         self.path = plan.query_path(N, Fin, K, Fout)
         fb, bb = plan.workspace_bytes(N, Fin, K, Fout)
         M = plan.M
         f32 = dict(device=dev, dtype=torch.float32)
-        if basis_layout == "auto":
-            basis_layout = "orders" if plan.basis_elems(N, Fin, K, Fout, "orders") else "rows"
         if basis_layout == "orders":
             if plan.basis_elems(N, Fin, K, Fout, "orders") is None:
                 raise ValueError("orders basis layout does not apply to this shape "

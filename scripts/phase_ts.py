@@ -73,6 +73,24 @@ def main():
                    for k in names}
             res[f"{layout}:{name}"] = {"kernel_us": round(e0.elapsed_time(e1) / 20 * 1e3, 2),
                                        "phase_us_median_max": med}
+    # backward ablations (rows layout; outputs wrong): the fused dW's MFMAs
+    # or its operand loads skipped during the recurrence
+    h.cg_debug_set_flags.argtypes = [ctypes.c_int]
+    r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
+    for tag, flags in (("bwd_no_dw_mfma", 64 << 8), ("bwd_no_dw_load", 128 << 8),
+                       ("bwd_no_dw_both", 192 << 8)):
+        h.cg_debug_set_flags(flags)
+        lines = []
+        for _ in range(5):
+            buf.zero_()
+            h.cg_debug_set_ts(buf.data_ptr())
+            r.backward(dy, W)
+            torch.cuda.synchronize()
+            h.cg_debug_set_ts(None)
+            lines.append(timeline(buf.cpu().numpy(), BWD))
+        h.cg_debug_set_flags(0)
+        res[f"rows:{tag}"] = {"kernel_us": None, "phase_us_median_max": {
+            k: [round(float(np.median([ln[k][i] for ln in lines])), 2) for i in (0, 1)] for k in BWD}}
     print(json.dumps(res, indent=1))
 
 
