@@ -263,16 +263,34 @@ def main():
         ar_args = (comm.handle, runner.dW.data_ptr(), runner.dW.numel(), stream)
 
     # No exchange step (one GPU): the Adam update rides on the dW reduction
-    # (cg_cheb_backward_adam) instead of a separate launch.
+    # (cg_cheb_backward_adam) instead of a separate launch.  With an exchange
+    # (N > 1), the update of the all-reduced dW is applied by the NEXT step's
+    # forward (cg_cheb_forward_adam: W, m, v double-buffered, no Adam launch);
+    # step i's forward applies step i-1's gradient, so every timed step still
+    # does one forward, backward, all-reduce and Adam update.
     fuse_adam = not exchange and not args.unfused_adam
+    fwd_adam = exchange and not args.unfused_adam
+    Wb = [W, torch.empty_like(W)]
+    mb = [m_adam, torch.zeros_like(W)]
+    vb = [v_adam, torch.zeros_like(W)]
 
     def step(i):
-        runner.forward(x, W, stream=stream)
+        if fwd_adam:
+            if i == 0:
+                runner.forward(x, Wb[0], stream=stream)
+            else:
+                pi, ci = (i - 1) % 2, i % 2
+                runner.forward_adam(x, Wb[pi], runner.dW, mb[pi], vb[pi], Wb[ci], mb[ci], vb[ci],
+                                    i, grad_scale=1.0 / world, stream=stream)
+            Wc = Wb[i % 2]
+        else:
+            Wc = W
+            runner.forward(x, W, stream=stream)
         if fuse_adam:
             runner.backward_adam(dy, W, m_adam, v_adam, i + 1, grad_scale=1.0 / world,
                                  stream=stream)
             return
-        runner.backward(dy, W, stream=stream)
+        runner.backward(dy, Wc, stream=stream)
         if exchange:
             if comm is not None:
                 st = ar_fn(*ar_args)
@@ -280,9 +298,10 @@ def main():
                     _lib.check("cg_allreduce_sum_f32", st)
             else:
                 dist.all_reduce(runner.dW, op=dist.ReduceOp.SUM)
-        st = adam(*adam_args, i + 1, scale, stream)
-        if st:
-            _lib.check("cg_adam_update", st)
+        if not fwd_adam:
+            st = adam(*adam_args, i + 1, scale, stream)
+            if st:
+                _lib.check("cg_adam_update", st)
 
     for i in range(args.warmup):
         step(i)
@@ -346,7 +365,8 @@ def main():
                    "parallelism": f"dp{world}",
                    "allreduce": (args.allreduce if exchange else None),
                    "adam": ("fused into the dW reduction (cg_cheb_backward_adam)" if fuse_adam
-                            else "cg_adam_update")},
+                            else "applied by the next step's forward (cg_cheb_forward_adam)"
+                            if fwd_adam else "cg_adam_update")},
         "roofline": {"bound": "hbm", "kernel": kern[dom]["kernel"],
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4),

@@ -63,6 +63,10 @@ _SIGNATURES = {
                                 _vp, _vp, _vp, _c_sz, _vp], _c_int),
     "cg_cheb_backward_layout": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i32, _vp,
                                  _vp, _vp, _c_i32, _vp, _vp, _vp, _c_sz, _vp], _c_int),
+    "cg_cheb_forward_adam": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp,
+                              ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                              _c_i32, ctypes.c_float, _vp, _vp, _vp, _c_i32, _vp, _vp, _vp, _c_sz,
+                              _vp], _c_int),
     "cg_cheb_backward_adam_layout": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp,
                                       _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float,
                                       ctypes.c_float, ctypes.c_float, _c_i32, ctypes.c_float, _vp,

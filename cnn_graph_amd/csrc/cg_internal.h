@@ -160,6 +160,17 @@ struct FastFwdArgs {
   float* y;
   int bord;  // 0: basis [N*M][Fin*K]; else the orders layout [N][Fin*K][bord] (bord = Mb)
   unsigned long long* ts;  // ablation build: phase timestamps (CG_TS), else NULL
+  // Adam in the prologue (cg_cheb_forward_adam), when ad_grad != NULL: the
+  // contraction uses W' = ApplyAdam(W, grad) computed by every workgroup
+  // alike; workgroup 0 stores W', m', v' (out-of-place: the others still read
+  // W, m, v)
+  const float* ad_grad;
+  const float* ad_m;
+  const float* ad_v;
+  float* ad_W;
+  float* ad_mo;
+  float* ad_vo;
+  float ad_lr_t, ad_b1, ad_b2, ad_eps, ad_scale;
 };
 struct FastBwdArgs {
   int M, Fin, K, Fout, Mp, dbg;
@@ -343,6 +354,22 @@ struct AdamStep {
   float* v;
   float lr_t, beta1, beta2, eps, grad_scale;
 };
+// TF-1.x ApplyAdam on one element (lib/graph_model.py:293-298), one rounding
+// per operation (no FMA contraction, as TF's CPU functor): the single
+// definition k_adam, k_reduce_slabs_adam and the Adam-in-forward prologue of
+// cheb_fwd_fast share, so all three agree bitwise.
+struct AdamElem {
+  float p, m, v;
+};
+__device__ __forceinline__ AdamElem adam_math(float p0, float m0, float v0, float grad,
+                                              float grad_scale, float lr_t, float beta1,
+                                              float beta2, float eps) {
+#pragma clang fp contract(off)
+  const float g = grad * grad_scale;
+  const float mi = m0 + (g - m0) * (1.f - beta1);
+  const float vi = v0 + (g * g - v0) * (1.f - beta2);
+  return AdamElem{p0 - lr_t * mi / (sqrtf(vi) + eps), mi, vi};
+}
 // grad[i] = sum_z slab[z][i] in k_reduce_slabs' order (bitwise the same dW),
 // then the k_adam update of element i, in one launch.
 hipError_t launch_reduce_slabs_adam(const float* slab, int nslab, int64_t count, float* grad,

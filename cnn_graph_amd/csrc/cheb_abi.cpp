@@ -600,10 +600,22 @@ int cg_cheb_workspace_bytes(const cg_plan* plan, int32_t N, int32_t Fin, int32_t
 }  // extern "C"
 
 namespace {
+// Adam applied to W by the forward that consumes it (cg_cheb_forward_adam)
+struct FwdAdam {
+  const float* grad;
+  const float* m;
+  const float* v;
+  float* W_out;
+  float* m_out;
+  float* v_out;
+  float lr_t, beta1, beta2, eps, grad_scale;
+};
+
 // forward with the residual / activation epilogue y = act(basis W + res)
 int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout, const float* x,
                  const float* W, const float* res, int act, float* basis, float* y, void* workspace,
-                 size_t ws_bytes, void* stream, int layout = CG_BASIS_ROWS) {
+                 size_t ws_bytes, void* stream, int layout = CG_BASIS_ROWS,
+                 const FwdAdam* fa = nullptr) {
   int rc = check_shape(plan, N, Fin, K, Fout);
   if (rc) return rc;
   if ((rc = check_layout(plan, Fin, K, Fout, layout))) return rc;
@@ -617,8 +629,21 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
   if ((rc = choose_path(plan, Fin, K, Fout, false, &path))) return rc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int M = plan->M;
+  const bool fast_fwd =
+      layout == CG_BASIS_ORDERS || (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, false));
+  if (fa && !fast_fwd) {
+    // other kernels: the same update out of place by k_adam, then the forward on W'
+    const size_t nb = size_t(Fin) * K * Fout * sizeof(float);
+    CG_HIP(hipMemcpyAsync(fa->W_out, W, nb, hipMemcpyDeviceToDevice, s));
+    CG_HIP(hipMemcpyAsync(fa->m_out, fa->m, nb, hipMemcpyDeviceToDevice, s));
+    CG_HIP(hipMemcpyAsync(fa->v_out, fa->v, nb, hipMemcpyDeviceToDevice, s));
+    CG_HIP(cg::launch_adam(fa->W_out, fa->grad, fa->m_out, fa->v_out, int64_t(Fin) * K * Fout,
+                           fa->lr_t, fa->beta1, fa->beta2, fa->eps, fa->grad_scale, s));
+    W = fa->W_out;
+    fa = nullptr;
+  }
 
-  if (layout == CG_BASIS_ORDERS || (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, false))) {
+  if (fast_fwd) {
     cg::FastFwdArgs a{};
     a.M = M;
     a.Fin = Fin;
@@ -636,6 +661,20 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
 #ifdef CG_DEBUG
     a.ts = cg::g_debug_ts;
 #endif
+    if (fa) {
+      a.W = W;
+      a.ad_grad = fa->grad;
+      a.ad_m = fa->m;
+      a.ad_v = fa->v;
+      a.ad_W = fa->W_out;
+      a.ad_mo = fa->m_out;
+      a.ad_vo = fa->v_out;
+      a.ad_lr_t = fa->lr_t;
+      a.ad_b1 = fa->beta1;
+      a.ad_b2 = fa->beta2;
+      a.ad_eps = fa->eps;
+      a.ad_scale = fa->grad_scale;
+    }
     CG_HIP(cg::launch_fast_forward(fast_geom(plan, Fin, K, Fout), N, a, s));
     return ok();
   }
@@ -981,6 +1020,35 @@ int cg_cheb_forward_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int
                            size_t ws_bytes, void* stream) {
   return forward_impl(plan, N, Fin, K, Fout, x, W, residual, act, basis, y, workspace, ws_bytes,
                       stream, layout);
+}
+
+int cg_cheb_forward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                         const float* x, const float* W, const float* grad, const float* m,
+                         const float* v, float lr, float beta1, float beta2, float eps,
+                         int32_t step, float grad_scale, float* W_out, float* m_out, float* v_out,
+                         int32_t layout, float* basis, float* y, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  if (!W || !grad || !m || !v || !W_out || !m_out || !v_out || step < 1 || !y)
+    return fail(CG_ERR_ARG, "cheb_forward_adam: W, grad, m, v, W_out, m_out, v_out, y required "
+                            "and step >= 1");
+  // every workgroup reads W, m, v while workgroup 0 writes W', m', v': the
+  // outputs must not alias any input
+  const void* outs[3] = {W_out, m_out, v_out};
+  const void* ins[4] = {W, grad, m, v};
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 4; ++j)
+      if (outs[i] == ins[j])
+        return fail(CG_ERR_ARG, "cheb_forward_adam: W_out, m_out, v_out must not alias the inputs");
+    for (int j = i + 1; j < 3; ++j)
+      if (outs[i] == outs[j])
+        return fail(CG_ERR_ARG, "cheb_forward_adam: W_out, m_out, v_out must be distinct");
+  }
+  FwdAdam fa{grad, m, v, W_out, m_out, v_out,
+             float(double(lr) * std::sqrt(1.0 - std::pow(double(beta2), step)) /
+                   (1.0 - std::pow(double(beta1), step))),
+             beta1, beta2, eps, grad_scale};
+  return forward_impl(plan, N, Fin, K, Fout, x, W, nullptr, CG_ACT_NONE, basis, y, workspace,
+                      ws_bytes, stream, layout, &fa);
 }
 
 int cg_cheb_backward_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,

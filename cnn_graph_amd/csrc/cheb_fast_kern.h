@@ -293,7 +293,20 @@ struct Fwd {
       mb[t] = A.E.mpos[tile * 32 + li] * REC_;
     }
     char* smem = ring;
-    for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = A.W ? A.W[i] : 0.f;
+    if (A.ad_grad) {  // W' = ApplyAdam(W, grad), identical in every workgroup
+      for (int i = tid; i < FinK * Fout; i += kT) {
+        const AdamElem e = adam_math(A.W[i], A.ad_m[i], A.ad_v[i], A.ad_grad[i], A.ad_scale,
+                                     A.ad_lr_t, A.ad_b1, A.ad_b2, A.ad_eps);
+        s_W[i] = e.p;
+        if (blockIdx.x == 0) {
+          A.ad_W[i] = e.p;
+          A.ad_mo[i] = e.m;
+          A.ad_vo[i] = e.v;
+        }
+      }
+    } else {
+      for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = A.W ? A.W[i] : 0.f;
+    }
     // T_0 = x into ring slot 0 ([pos][0][fin]); zero record kept at 0
     const float* xn = A.x + size_t(n) * M * FV;
     for (int i = tid; i < M * FV; i += kT) {

@@ -106,20 +106,16 @@ __global__ __launch_bounds__(256) void k_avgpool_bwd(const float* __restrict__ d
 // m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ; p -= lr_t m / (sqrt(v) + eps)
 // with lr_t = lr sqrt(1-b2^t)/(1-b1^t) computed on the host (TF's ApplyAdam).
 // TF-1.x Adam on one element (lib/graph_model.py:293-298 via tf.train.AdamOptimizer);
-// shared by k_adam and k_reduce_slabs_adam so both round identically.
+// the arithmetic is cg_internal.h::adam_math, shared with cheb_fwd_fast's
+// Adam-in-forward prologue, so every Adam path rounds identically.
 __device__ __forceinline__ void adam_elem(float* __restrict__ param, float* __restrict__ m,
                                           float* __restrict__ v, int64_t i, float grad,
                                           float grad_scale, float lr_t, float beta1, float beta2,
                                           float eps) {
-#pragma clang fp contract(off)
-  // one rounding per operation (no FMA contraction), as TF's ApplyAdam CPU
-  // functor evaluates it; k_adam and k_reduce_slabs_adam therefore agree bitwise
-  const float g = grad * grad_scale;
-  const float mi = m[i] + (g - m[i]) * (1.f - beta1);
-  const float vi = v[i] + (g * g - v[i]) * (1.f - beta2);
-  m[i] = mi;
-  v[i] = vi;
-  param[i] = param[i] - lr_t * mi / (sqrtf(vi) + eps);
+  const AdamElem r = adam_math(param[i], m[i], v[i], grad, grad_scale, lr_t, beta1, beta2, eps);
+  m[i] = r.m;
+  v[i] = r.v;
+  param[i] = r.p;
 }
 
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ param,

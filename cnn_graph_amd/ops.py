@@ -224,6 +224,27 @@ class ChebRunner:
         _lib.check("cg_cheb_forward_layout", st)
         return self.y
 
+    def forward_adam(self, x: torch.Tensor, W: torch.Tensor, grad: torch.Tensor, m: torch.Tensor,
+                     v: torch.Tensor, W_out: torch.Tensor, m_out: torch.Tensor,
+                     v_out: torch.Tensor, step: int, lr: float = 1e-3, beta1: float = 0.9,
+                     beta2: float = 0.999, eps: float = 1e-8, grad_scale: float = 1.0,
+                     stream=None):
+        """The exchange step's Adam on W applied by the forward that consumes it
+        (cg_cheb_forward_adam): W_out, m_out, v_out = ApplyAdam(W, grad; m, v),
+        then y = chebyshev5(x; W_out).  Outputs out of place (double-buffer them)."""
+        shape = (self.Fin * self.K, self.Fout)
+        for name, t_ in (("W", W), ("grad", grad), ("m", m), ("v", v), ("W_out", W_out),
+                         ("m_out", m_out), ("v_out", v_out)):
+            _check_out(name, t_, shape)
+        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        st = _lib.lib().cg_cheb_forward_adam(
+            self.plan.handle, self.N, self.Fin, self.K, self.Fout, x.data_ptr(), W.data_ptr(),
+            grad.data_ptr(), m.data_ptr(), v.data_ptr(), lr, beta1, beta2, eps, step, grad_scale,
+            W_out.data_ptr(), m_out.data_ptr(), v_out.data_ptr(), self._lay,
+            self.basis.data_ptr(), self.y.data_ptr(), self.fws.data_ptr(), self.fwd_bytes, s)
+        _lib.check("cg_cheb_forward_adam", st)
+        return self.y
+
     def backward(self, dy: torch.Tensor, W: torch.Tensor, need_dx: bool = True, stream=None):
         s = stream if stream is not None else torch.cuda.current_stream(dy.device).cuda_stream
         st = self._bwd(self.plan.handle, self.N, self.Fin, self.K, self.Fout, dy.data_ptr(), None, 0,

@@ -340,6 +340,21 @@ int cg_cheb_backward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int3
                           float* m, float* v, float lr, float beta1, float beta2, float eps,
                           int32_t step, float grad_scale, void* workspace, size_t ws_bytes,
                           void* stream);
+/* The exchange step's Adam moved into the forward that consumes it (data-parallel
+ * step: forward, backward, dW all-reduce, then this call of the NEXT step):
+ *   W_out = ApplyAdam(W, grad * grad_scale; m, v) -> m_out, v_out  (lib/graph_model.py:293-298)
+ *   basis, y = chebyshev5(x; W_out)                                (lib/graph_conv.py:155-176)
+ * The fast kernels apply the update in their prologue (every workgroup computes
+ * the same W_out; no separate Adam launch); other paths run k_adam first.  W_out,
+ * m_out, v_out are written out of place and must not alias W, grad, m, v
+ * (double-buffer them across steps).  Bitwise the result of cg_adam_update on
+ * copies of W, m, v followed by cg_cheb_forward_layout. */
+int cg_cheb_forward_adam(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
+                         const float* x, const float* W, const float* grad, const float* m,
+                         const float* v, float lr, float beta1, float beta2, float eps,
+                         int32_t step, float grad_scale, float* W_out, float* m_out, float* v_out,
+                         int32_t layout, float* basis, float* y, void* workspace,
+                         size_t ws_bytes, void* stream);
 /* The same with the basis in a chosen layout (CG_BASIS_*, see cg_cheb_basis_elems). */
 int cg_cheb_backward_adam_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                                  int32_t layout, const float* dy, const float* basis, float* W,

@@ -126,3 +126,23 @@ def test_basis_layout_entry_points_validate(built_lib):
     assert h.cg_cheb_backward_layout(None, 1, 1, 2, 1, None, None, 7, _lib.CG_BASIS_ORDERS, None,
                                      None, None, 0, None, None, None, 0, None) == _lib.CG_ERR_ARG
     assert "activation" in h.cg_last_error().decode()
+
+
+def test_forward_adam_validates(built_lib):
+    """cg_cheb_forward_adam rejects missing operands and aliased outputs before
+    any device work."""
+    h = _lib.lib()
+    p, q, r = ctypes.c_void_p(4096), ctypes.c_void_p(8192), ctypes.c_void_p(12288)
+    g, m, v = ctypes.c_void_p(16384), ctypes.c_void_p(20480), ctypes.c_void_p(24576)
+    y = ctypes.c_void_p(28672)
+    assert h.cg_cheb_forward_adam(None, 1, 1, 2, 1, None, None, None, None, None, 1e-3, 0.9, 0.999,
+                                  1e-8, 1, 1.0, None, None, None, 0, None, None, None, 0,
+                                  None) == _lib.CG_ERR_ARG
+    # W_out aliasing W
+    assert h.cg_cheb_forward_adam(None, 1, 1, 2, 1, None, p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 1,
+                                  1.0, p, q, r, 0, None, y, None, 0, None) == _lib.CG_ERR_ARG
+    assert "alias" in h.cg_last_error().decode()
+    # m_out == v_out
+    assert h.cg_cheb_forward_adam(None, 1, 1, 2, 1, None, p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 1,
+                                  1.0, q, r, r, 0, None, y, None, 0, None) == _lib.CG_ERR_ARG
+    assert "distinct" in h.cg_last_error().decode()
