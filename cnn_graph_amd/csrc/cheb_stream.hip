@@ -199,7 +199,9 @@ __global__ __launch_bounds__(256) void k_cheb_step(ChebStepArgs a, StepGeom g) {
 // Last forward step with the basis assembly staged through LDS: each wave
 // writes its rows' [fin][k] basis rows into LDS, then stores them with
 // coalesced 4-B lane stores (consecutive rows are one contiguous span in the
-// natural row order; with rperm each row's Fin*K floats are).
+// natural row order; with rperm each row's Fin*K floats are).  LDS rows are
+// Fin*K + 1 floats apart (odd): with Fin*K a multiple of 32 (the ResGNN hidden
+// layers, 32 x 20) an unpadded stride put every row of a wave in one bank.
 template <int VEC>
 __global__ __launch_bounds__(256) void k_cheb_last(ChebStepArgs a, StepGeom g) {
 #pragma clang fp contract(off)
@@ -209,7 +211,8 @@ __global__ __launch_bounds__(256) void k_cheb_last(ChebStepArgs a, StepGeom g) {
   int n, rb;
   block_coords(g, &n, &rb);
   const int FinK = a.Fin * a.K;
-  float* ws = stage + wave * g.rpw * FinK;
+  const int ls = FinK + 1;  // LDS row stride
+  float* ws = stage + wave * g.rpw * ls;
   const int rsub = lane / g.lpr, lc = lane - rsub * g.lpr;
   const int ri0 = (rb * 4 + wave) * g.rpw;
   const int ri = ri0 + rsub;
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(256) void k_cheb_last(ChebStepArgs a, StepGeom g) {
     const int j0 = a.rowptr[r], j1 = a.rowptr[r + 1];
     const int64_t sbase = int64_t(n) * a.M * a.Fin;
     const int64_t rbase = sbase + int64_t(r) * a.Fin;
-    float* srow = ws + rsub * FinK;
+    float* srow = ws + rsub * ls;
     for (int f0 = lc * VEC; f0 < a.Fin; f0 += g.lpr * VEC) {
       const typename V::T acc = row_spmm<VEC>(a.col, a.val, j0, j1, a.Tp + sbase, a.Fin, f0);
       const typename V::T o = (a.k >= 2) ? V::two_minus(acc, V::ld(a.Tpp + rbase + f0)) : acc;
@@ -238,11 +241,14 @@ __global__ __launch_bounds__(256) void k_cheb_last(ChebStepArgs a, StepGeom g) {
   if (!a.rperm) {
     float* dst = a.basis + (int64_t(n) * a.M + ri0) * FinK;
     const int count = nrows * FinK;
-    for (int e = lane; e < count; e += 64) dst[e] = ws[e];
+    for (int e = lane; e < count; e += 64) {
+      const int q = e / FinK;
+      dst[e] = ws[e + q];  // row q at q * (FinK + 1)
+    }
   } else {
     for (int q = 0; q < nrows; ++q) {
       float* dst = a.basis + (int64_t(n) * a.M + a.rperm[ri0 + q]) * FinK;
-      for (int e = lane; e < FinK; e += 64) dst[e] = ws[q * FinK + e];
+      for (int e = lane; e < FinK; e += 64) dst[e] = ws[q * ls + e];
     }
   }
 }
@@ -572,8 +578,17 @@ hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val,
   const int vec = (Fin % 4 == 0) ? 4 : 1;
   const StepGeom g = step_geom(N, M, Fin, vec);
   const dim3 grid(unsigned(int64_t(N) * g.rb)), block(256);
-  const size_t stage = size_t(4) * g.rpw * size_t(Fin) * K * sizeof(float);
-  if (last && stage <= size_t(64) * 1024) {
+  const size_t stage = size_t(4) * g.rpw * (size_t(Fin) * K + 1) * sizeof(float);
+  // up to the CU's whole LDS: the per-lane scattered basis stores of
+  // k_cheb_step<., true> are ~10x slower (config R's 32 x 20 hidden layers:
+  // 835 us per call, profiles/r02_resgnn)
+  static const hipError_t attr4 = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&k_cheb_last<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      kLdsBytes);
+  static const hipError_t attr1 = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&k_cheb_last<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      kLdsBytes);
+  if (last && stage <= size_t(kLdsBytes) && attr4 == hipSuccess && attr1 == hipSuccess) {
     if (vec == 4) hipLaunchKernelGGL((k_cheb_last<4>), grid, block, stage, s, a, g);
     else hipLaunchKernelGGL((k_cheb_last<1>), grid, block, stage, s, a, g);
   } else if (vec == 4) {

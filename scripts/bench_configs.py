@@ -104,6 +104,30 @@ def lstm_config(dev, T=12, N=128, Fin=2, H=32, K=3, hconv="auto"):
             "samples_per_s": round(N / (fb * 1e-3), 1)}
 
 
+def resgnn_config(dev, N=100, Fin=2, nfilter=32, K=20, nres=4):
+    """ResGNN training step (§8f-1, lib/graph_model.py:246-310 with
+    lib/graph_conv.py:305-330): the humanflow-ln-period shape (M = 1024,
+    nfilter 32, 4 residual layers, K 20, batch 100) on config E's
+    1024-vertex graph -- 2*nres + 2 = 10 chebyshev5 calls per forward, the
+    hidden ones with Fin = Fout = 32 (streaming path)."""
+    from cnn_graph_amd.model import ResGNN
+    with np.load(os.path.join(ROOT, "tests", "golden", "golden_E.npz"), allow_pickle=False) as z:
+        M = int(z["M"])
+        Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
+    L = (Lt + scipy.sparse.identity(M, dtype=np.float32, format="csr")).tocsr()
+    model = ResGNN(L, N=N, Fin=Fin, nfilter=nfilter, K=K, nres_layer_count=nres, device=dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    x = torch.rand((N, M, Fin), device=dev, generator=g)
+    labels = torch.rand((N, M, 2), device=dev, generator=g)
+    paths = sorted({model.plan.query_path(N, fi, K, fo) for fi, fo in
+                    ((Fin, nfilter), (nfilter, nfilter), (nfilter, 2))})
+    ms = ev_ms(lambda: model.train_step(x, labels), reps=5)
+    return {"config": "R", "M": M, "N": N, "Fin": Fin, "nfilter": nfilter, "K": K,
+            "nres_layer_count": nres, "filter_calls_per_step": 2 * nres + 2, "paths": paths,
+            "step_ms": round(ms, 3), "samples_per_s": round(N / (ms * 1e-3), 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["C1", "C2", "D", "E"])
@@ -128,6 +152,8 @@ def main():
             out = lstm_config(dev)
         elif name == "E_unfused":
             out = lstm_config(dev, hconv="unfused")
+        elif name == "R":
+            out = resgnn_config(dev)
         else:
             raise SystemExit(f"unknown config {name}")
         print(json.dumps(out), flush=True)
