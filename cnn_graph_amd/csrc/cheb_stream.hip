@@ -620,8 +620,10 @@ static int rowgemm_kc2(int Kc) {
 bool rowgemm_ok(int Kc, int lda, int Nc) {
   const int KC2 = rowgemm_kc2(Kc);
   const int NT = (Nc + 31) / 32;
-  return Kc >= 2 && Kc <= 256 && Nc >= 1 && NT <= 8 && lda >= Kc &&
-         size_t(2) * KC2 * NT * 32 * 4 <= size_t(64) * 1024;
+  // (B staged whole in LDS: up to the CU's 160 KB, e.g. the ResGNN hidden
+  // layers' y = basis W with Kc = 32 x 20 = 640, 80 KB)
+  return Kc >= 2 && Kc <= 1024 && Nc >= 1 && NT <= 8 && lda >= Kc &&
+         size_t(2) * KC2 * NT * 32 * 4 <= size_t(kLdsBytes);
 }
 
 hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
@@ -636,6 +638,24 @@ hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const floa
   const int64_t ntiles = (R + 127) / 128;
   const unsigned gx = unsigned(ntiles < 1024 ? ntiles : 1024);
   const dim3 grid(gx, unsigned(planes)), block(256);
+  if (lds > size_t(64) * 1024) {
+    static hipError_t attr[8] = {};
+    static bool set = false;
+    if (!set) {
+      const void* ks[8] = {reinterpret_cast<const void*>(&k_rowgemm<1>),
+                           reinterpret_cast<const void*>(&k_rowgemm<2>),
+                           reinterpret_cast<const void*>(&k_rowgemm<3>),
+                           reinterpret_cast<const void*>(&k_rowgemm<4>),
+                           reinterpret_cast<const void*>(&k_rowgemm<5>),
+                           reinterpret_cast<const void*>(&k_rowgemm<6>),
+                           reinterpret_cast<const void*>(&k_rowgemm<7>),
+                           reinterpret_cast<const void*>(&k_rowgemm<8>)};
+      for (int q = 0; q < 8; ++q)
+        attr[q] = hipFuncSetAttribute(ks[q], hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+      set = true;
+    }
+    if (attr[(NT < 8 ? NT : 8) - 1] != hipSuccess) return attr[(NT < 8 ? NT : 8) - 1];
+  }
   switch (NT) {
     case 1: hipLaunchKernelGGL(k_rowgemm<1>, grid, block, lds, s, a); break;
     case 2: hipLaunchKernelGGL(k_rowgemm<2>, grid, block, lds, s, a); break;
