@@ -15,7 +15,7 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeou
 tail -1 $OUT/pytest_gpu.txt
 timeout -k 10 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 10 > $OUT/bench.json 2>&1 || { echo BENCH_FAIL; tail -30 $OUT/bench.json; exit 1; }
 tail -1 $OUT/bench.json
-timeout -k 10 400 python scripts/bench_configs.py C1 C2 D E > $OUT/configs.jsonl 2>&1 || { echo CFG_FAIL; tail -20 $OUT/configs.jsonl; exit 1; }
+timeout -k 10 500 python scripts/bench_configs.py C1 C2 D E R > $OUT/configs.jsonl 2>&1 || { echo CFG_FAIL; tail -20 $OUT/configs.jsonl; exit 1; }
 grep config $OUT/configs.jsonl
 bash scripts/prof_pmc.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { echo PMC_FAIL; tail -20 $OUT/pmc.log; exit 1; }
 tail -5 $OUT/pmc.log
