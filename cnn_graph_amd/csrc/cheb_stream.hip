@@ -48,10 +48,15 @@ struct StepGeom {
   int lpr;      // lanes per row
   int rpw;      // rows per wave (64 / lpr)
   int rb;       // row blocks (of 4 waves) per sample
-  int xcd_map;  // 1: sample-per-XCD block mapping (N % 8 == 0)
+  int xcd_map;  // 1: sample-per-XCD block mapping
+  int N;        // samples; with xcd_map the grid covers 8 * ceil(N / 8) of
+                // them and the blocks of samples n >= N exit at once
+  unsigned grid;  // blocks to launch
 };
 
-__device__ __forceinline__ void block_coords(const StepGeom g, int* n, int* rb) {
+// Block -> (sample, row block).  Returns false for the padding blocks of the
+// sample-per-XCD mapping (N not a multiple of 8), which exit immediately.
+__device__ __forceinline__ bool block_coords(const StepGeom g, int* n, int* rb) {
   const int i = blockIdx.x;
   if (g.xcd_map) {
     const int x = i & 7, q = i >> 3;
@@ -61,6 +66,7 @@ __device__ __forceinline__ void block_coords(const StepGeom g, int* n, int* rb) 
     *n = i / g.rb;
     *rb = i % g.rb;
   }
+  return *n < g.N;
 }
 
 template <int VEC>
@@ -167,7 +173,7 @@ __global__ __launch_bounds__(256) void k_cheb_step(ChebStepArgs a, StepGeom g) {
   typedef Vec<VEC> V;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int n, rb;
-  block_coords(g, &n, &rb);
+  if (!block_coords(g, &n, &rb)) return;
   const int rsub = lane / g.lpr, lc = lane - rsub * g.lpr;
   if (rsub >= g.rpw) return;
   const int ri = (rb * 4 + wave) * g.rpw + rsub;
@@ -209,7 +215,7 @@ __global__ __launch_bounds__(256) void k_cheb_last(ChebStepArgs a, StepGeom g) {
   extern __shared__ float stage[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int n, rb;
-  block_coords(g, &n, &rb);
+  if (!block_coords(g, &n, &rb)) return;
   const int FinK = a.Fin * a.K;
   const int ls = FinK + 1;  // LDS row stride
   float* ws = stage + wave * g.rpw * ls;
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(256) void k_clenshaw_step(ClenArgs a, StepGeom g) {
   typedef Vec<VEC> V;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int n, rb;
-  block_coords(g, &n, &rb);
+  if (!block_coords(g, &n, &rb)) return;
   const int rsub = lane / g.lpr, lc = lane - rsub * g.lpr;
   if (rsub >= g.rpw) return;
   const int ri = (rb * 4 + wave) * g.rpw + rsub;
@@ -413,9 +419,15 @@ StepGeom step_geom(int N, int M, int Fin, int vec) {
   // sample-per-XCD mapping keeps each XCD's gathers inside one sample slab in
   // its own 4 MB L2; slabs larger than that are better shared by all XCDs at
   // once (all blocks of sample n before sample n+1) so the one slab being
-  // gathered stays in the 256 MB Infinity Cache
+  // gathered stays in the 256 MB Infinity Cache.  N not a multiple of 8 (the
+  // humanflow ResGNN's batch of 100) pads the grid to 8 * ceil(N / 8) samples
+  // rather than falling back to the sample-major order, which spreads every
+  // sample's blocks over all 8 XCDs (each L2 then holds all N slabs)
   const int64_t slab = int64_t(M) * Fin * 4;
-  g.xcd_map = (N % 8 == 0 && slab <= (int64_t(2) << 20)) ? 1 : 0;
+  g.xcd_map = (slab <= (int64_t(2) << 20)) ? 1 : 0;
+  g.N = N;
+  const int64_t ns = g.xcd_map ? (int64_t(N) + 7) / 8 * 8 : int64_t(N);
+  g.grid = unsigned(ns * g.rb);
   return g;
 }
 
@@ -577,7 +589,7 @@ hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val,
                  int64_t(N) * M * Fin, basis, M, Fin, K, k};
   const int vec = (Fin % 4 == 0) ? 4 : 1;
   const StepGeom g = step_geom(N, M, Fin, vec);
-  const dim3 grid(unsigned(int64_t(N) * g.rb)), block(256);
+  const dim3 grid(g.grid), block(256);
   const size_t stage = size_t(4) * g.rpw * (size_t(Fin) * K + 1) * sizeof(float);
   // up to the CU's whole LDS: the per-lane scattered basis stores of
   // k_cheb_step<., true> are ~10x slower (config R's 32 x 20 hidden layers:
@@ -607,7 +619,7 @@ hipError_t launch_clenshaw(const int* trowptr, const int* tcol, const float* tva
   ClenArgs a{trowptr, tcol, tval, rperm, Gn1, Gn2, Gout, Dk, M, Fin, K, k, dx_acc};
   const int vec = (Fin % 4 == 0) ? 4 : 1;
   const StepGeom g = step_geom(N, M, Fin, vec);
-  const dim3 grid(unsigned(int64_t(N) * g.rb)), block(256);
+  const dim3 grid(g.grid), block(256);
   if (vec == 4) hipLaunchKernelGGL((k_clenshaw_step<4>), grid, block, 0, s, a, g);
   else hipLaunchKernelGGL((k_clenshaw_step<1>), grid, block, 0, s, a, g);
   return hipGetLastError();

@@ -41,10 +41,14 @@ def golden_L(name):
 
 
 @pytest.mark.parametrize("path,Fin,Fout", [("resident", 1, 16), ("resident", 4, 32),
-                                           ("resident", 3, 40), ("stream", 8, 32)])
+                                           ("resident", 3, 40), ("stream", 8, 32),
+                                           ("stream", 32, 32), ("stream", 32, 40),
+                                           ("stream", 32, 64)])
 def test_forward_epilogue_and_backward_ex(dev, path, Fin, Fout):
     """y = relu(basis W + res) (fast / classic / streaming kernels), then the
-    backward through it with dx accumulation."""
+    backward through it with dx accumulation.  Fin = 32 on the streaming path:
+    the ResGNN hidden-layer shape (row GEMM epilogue, one or two Fout tiles,
+    Fout = 40 a partial tile)."""
     from cnn_graph_amd import ops
     from cnn_graph_amd.plan import ChebPlan
     L, c = golden_L("golden_B.npz")
