@@ -21,8 +21,8 @@ PATHS = {"auto": CG_PATH_AUTO, "resident": CG_PATH_RESIDENT, "stream": CG_PATH_S
 CG_VARIANT_AUTO, CG_VARIANT_CLASSIC, CG_VARIANT_UNFUSED_DW, CG_VARIANT_NARROW = 0, 1, 2, 3
 VARIANTS = {"auto": CG_VARIANT_AUTO, "classic": CG_VARIANT_CLASSIC,
             "unfused_dw": CG_VARIANT_UNFUSED_DW, "narrow": CG_VARIANT_NARROW}
-CG_BASIS_ROWS, CG_BASIS_ORDERS = 0, 1
-BASIS_LAYOUTS = {"rows": CG_BASIS_ROWS, "orders": CG_BASIS_ORDERS}
+CG_BASIS_ROWS, CG_BASIS_ORDERS, CG_BASIS_PLANES = 0, 1, 2
+BASIS_LAYOUTS = {"rows": CG_BASIS_ROWS, "orders": CG_BASIS_ORDERS, "planes": CG_BASIS_PLANES}
 
 
 class CGError(RuntimeError):

@@ -249,10 +249,13 @@ bool rowgemm_ok(int Kc, int lda, int Nc);
 // pfin > 0 (planes == 1, no epilogue): one pass over A computes Nc = P*pfin
 // columns, column jj being column jj % pfin of plane jj / pfin (B and C alike),
 // so A is read once for all planes instead of once per plane.
+// apl_fin > 0 (planes == 1): A is a basis in the planes layout, K = bmapK
+// planes of [R][apl_fin] apl_stride floats apart (inner index kk = k*apl_fin +
+// fin), B the [Fin*K][Nc] weight in its own row order fin*K + k.
 hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
                           int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
                           int64_t c_plane, hipStream_t s, const float* res = nullptr, int act = 0,
-                          int pfin = 0);
+                          int pfin = 0, int apl_fin = 0, int64_t apl_stride = 0, int bmapK = 0);
 // remapK > 0: write C in the k-major [remapK][Mg][Ng/remapK] layout instead
 // (column fin*K + k -> plane k), splits must be 1.
 hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, const float* A,
@@ -261,8 +264,11 @@ hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, c
 // dW = basis^T dy as per-chunk partial slabs ([dw_chunks(R)][FinK][Fout]),
 // R = N*M basis rows; reduce with launch_reduce_slabs.
 int dw_chunks(int64_t R);
+// pl_fin > 0: basis in the planes layout (K planes of [R][pl_fin], pl_stride
+// floats apart); the slabs keep the rows layout's [Fin*K][Fout] order.
 hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
-                           float* slab, hipStream_t s);
+                           float* slab, hipStream_t s, int pl_fin = 0, int64_t pl_stride = 0,
+                           int K = 0);
 // Number of K slices launch_gemm_f32 actually uses for `splits` requested.
 int gemm_effective_splits(int Kg, int splits);
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,

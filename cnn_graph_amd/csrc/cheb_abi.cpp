@@ -336,6 +336,20 @@ inline int32_t basis_mb(int32_t M) { return (M + 31) & ~31; }
 
 int check_layout(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout, int layout) {
   if (layout == CG_BASIS_ROWS) return CG_OK;
+  if (layout == CG_BASIS_PLANES) {
+    // the sample-major streaming path both ways (Fin >= 16 never takes the
+    // wide-column layout), planes whose 16-float chunks the row GEMM loads
+    int pf = 0, pb = 0;
+    const bool ok = Fin % 16 == 0 && K >= 2 && !choose_path(p, Fin, K, Fout, false, &pf) &&
+                    !choose_path(p, Fin, K, Fout, true, &pb) && pf == CG_PATH_STREAM &&
+                    pb == CG_PATH_STREAM && cg::rowgemm_ok(Fin * K, Fin * K, Fout);
+    if (!ok)
+      return fail(CG_ERR_UNSUPPORTED,
+                  "planes basis layout needs the sample-major streaming path forward and "
+                  "backward, Fin a multiple of 16 and K >= 2 (M=%d Fin=%d K=%d Fout=%d)",
+                  p->M, Fin, K, Fout);
+    return CG_OK;
+  }
   if (layout != CG_BASIS_ORDERS) return fail(CG_ERR_ARG, "unknown basis layout %d", layout);
   // the fast forward without the basis staging (so it also serves shapes whose
   // staged basis would not fit in LDS) and the fused-dW fast backward
@@ -726,6 +740,16 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                                   M, N, K, s));
     else
       CG_HIP(cg::launch_wide_assemble(slots, int64_t(slot), N, M, Fin, K, basis, s));
+  } else if (layout == CG_BASIS_PLANES) {
+    // planes layout: T_k IS plane k of the basis (plane 0 a copy of x), every
+    // step writes its own plane, no assembly step (lib/graph_conv.py:159-169)
+    const int* rperm = (Fin >= 16) ? plan->rperm : nullptr;
+    auto P = [&](int k) { return basis + size_t(k) * slot; };
+    CG_HIP(hipMemcpyAsync(basis, x, slot * sizeof(float), hipMemcpyDeviceToDevice, s));
+    for (int k = 1; k < K; ++k)
+      CG_HIP(cg::launch_cheb_step(plan->rowptr, plan->col, plan->val, rperm, k == 1 ? x : P(k - 1),
+                                  k == 2 ? x : (k > 2 ? P(k - 2) : nullptr), P(k), x, nullptr,
+                                  nullptr, N, M, Fin, K, k, false, s));
   } else {
     // sample-major steps: T_0 = x, T_j (1 <= j <= K-2) in slots[j-1], the last
     // step writes the whole basis (lib/graph_conv.py:159-172)
@@ -739,7 +763,12 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                                   M, Fin, K, k, last, s));
     }
   }
-  if (y) {
+  if (y && layout == CG_BASIS_PLANES) {
+    // y = sum_k T_k W_k straight from the planes (row GEMM, A addressed per plane)
+    const int FinK = Fin * K;
+    CG_HIP(cg::launch_rowgemm(basis, int64_t(N) * M, FinK, FinK, W, Fout, 1, 0, 1, Fout, y, Fout, 0,
+                              s, res, act, 0, Fin, int64_t(slot), K));
+  } else if (y) {
     const int FinK = Fin * K;
     if (cg::rowgemm_ok(FinK, FinK, Fout)) {
       CG_HIP(cg::launch_rowgemm(basis, int64_t(N) * M, FinK, FinK, W, Fout, 1, 0, 1, Fout, y, Fout,
@@ -897,7 +926,9 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   if (!dW) return ok();
   if (fused) nslab_ready = N;
   if (!nslab_ready && !(cg::debug_flags() & (1 << 22)))  // ablation hook (debug build): skip dW
-    CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, s));
+    CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, s,
+                               layout == CG_BASIS_PLANES ? Fin : 0,
+                               layout == CG_BASIS_PLANES ? int64_t(R) * Fin : 0, K));
   const int nslab = nslab_ready ? nslab_ready : chunks;
   if (adam)  // reduction + optimizer step in one launch (no exchange in between)
     CG_HIP(cg::launch_reduce_slabs_adam(slabs, nslab, int64_t(FinK) * Fout, dW, *adam, s));

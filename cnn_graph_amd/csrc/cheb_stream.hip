@@ -283,6 +283,13 @@ struct RowGemmArgs {
   int pfin;          // > 0: ONE pass computes every plane -- column jj is
                      // (plane jj / pfin, column jj % pfin) of B and of C
   int vecA;          // A rows are 16-byte aligned (lda % 4 == 0): float4 loads
+  // A in the planes basis layout (apl_fin > 0): A[r][kk] =
+  // A[(kk / apl_fin) * apl_stride + r * apl_fin + kk % apl_fin] (order k =
+  // kk / apl_fin, channel kk % apl_fin; lda unused), and B row kk is row
+  // (kk % apl_fin) * bmapK + kk / apl_fin of the [Fin*K][Nc] weight
+  int apl_fin;
+  int64_t apl_stride;
+  int bmapK;
 };
 
 template <int NT>
@@ -295,9 +302,9 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
   for (int e = tid; e < KP * NP; e += 256) {
     const int kk = e / NP, j = e - kk * NP;
     // row kk of the padded operand: half 0 holds k < KC2, half 1 holds KC2 + (kk - KC2)
-    const int k = kk;
+    const int k = a.apl_fin > 0 ? (kk % a.apl_fin) * a.bmapK + kk / a.apl_fin : kk;
     float v = 0.f;
-    if (k < a.Kc && j < a.Nc) {
+    if (kk < a.Kc && j < a.Nc) {
       const int pp = a.pfin > 0 ? j / a.pfin : p;
       const int jj = a.pfin > 0 ? j - pp * a.pfin : j;
       v = a.B[pp * a.bs_p + int64_t(k) * a.bs_k + int64_t(jj) * a.bs_j];
@@ -312,7 +319,11 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
     const int64_t r0 = tile * 128 + wave * 32;
     if (r0 >= a.R) continue;
     const int64_t row = (r0 + i < a.R) ? r0 + i : a.R - 1;
-    const float* arow = a.A + row * a.lda;
+    const float* arow = a.A + row * (a.apl_fin > 0 ? a.apl_fin : a.lda);
+    // element kk of this row (planes layout: order kk / apl_fin's plane)
+    auto aptr = [&](int kk) -> const float* {
+      return a.apl_fin > 0 ? arow + (kk / a.apl_fin) * a.apl_stride + kk % a.apl_fin : arow + kk;
+    };
     f32x16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -323,9 +334,10 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
       const int k0 = kbeg + c0;
       const int nq = (a.KC2 - c0 < 16) ? a.KC2 - c0 : 16;  // (small Kc: no padded MFMAs)
       if (a.vecA && nq == 16 && k0 + 16 <= a.Kc) {
+        const float* ap = aptr(k0);  // 16 contiguous floats (host: apl_fin % 16 == 0)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(arow + k0 + 4 * q);
+          const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
           av[4 * q] = v.x;
           av[4 * q + 1] = v.y;
           av[4 * q + 2] = v.z;
@@ -333,7 +345,7 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
         }
       } else {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) av[q] = (q < nq && k0 + q < a.Kc) ? arow[k0 + q] : 0.f;
+        for (int q = 0; q < 16; ++q) av[q] = (q < nq && k0 + q < a.Kc) ? *aptr(k0 + q) : 0.f;
       }
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -506,10 +518,14 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int Mg, int Ng, int Kg, const 
 // through LDS, so the result is bitwise reproducible.  HBM-bound: it reads
 // basis + dy once (4*R*(FinK + Fout) bytes) and is meant to run on a side
 // stream concurrently with the latency-bound backward recurrence.
+// pl_fin > 0: the basis is in the planes layout (column jj = k*pl_fin + fin of
+// row r at basis[k*pl_stride + r*pl_fin + fin]); the slab keeps the rows
+// layout's column order fin*K + k.
 __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basis,
                                                   const float* __restrict__ dy, int64_t R,
                                                   int FinK, int Fout, int64_t rows_per_chunk,
-                                                  float* __restrict__ slab) {
+                                                  float* __restrict__ slab, int pl_fin,
+                                                  int64_t pl_stride, int K) {
   __shared__ float part[4][32][33];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, li = lane & 31;
@@ -518,6 +534,9 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
   const int j = jt * 32 + li, f = ft * 32 + li;
   const bool jv = j < FinK, fv = f < Fout;
   const int jc = jv ? j : FinK - 1, fc = fv ? f : Fout - 1;
+  // column jc of row rr at bcol + rr * bld
+  const float* bcol = pl_fin > 0 ? basis + int64_t(jc / pl_fin) * pl_stride + jc % pl_fin : basis + jc;
+  const int64_t bld = pl_fin > 0 ? pl_fin : FinK;
   const int64_t c0 = int64_t(blockIdx.x) * rows_per_chunk;
   const int64_t c1 = (c0 + rows_per_chunk < R) ? c0 + rows_per_chunk : R;
   const int64_t q = (((c1 - c0) + 3) / 4 + 1) & ~int64_t(1);  // even rows per wave
@@ -532,7 +551,7 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
     for (int u = 0; u < 8; ++u) {
       int64_t rr = rb + 2 * u + h;
       rr = rr < R ? rr : R - 1;
-      a[u] = basis[rr * FinK + jc];
+      a[u] = bcol[rr * bld];
       b[u] = dy[rr * Fout + fc];
     }
 #pragma unroll
@@ -549,7 +568,8 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
     const int row = e >> 5, col = e & 31;
     const float s = ((part[0][row][col] + part[1][row][col]) + part[2][row][col]) + part[3][row][col];
     const int jj = jt * 32 + row, ff = ft * 32 + col;
-    if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jj) * Fout + ff] = s;
+    const int jo = pl_fin > 0 ? (jj % pl_fin) * K + jj / pl_fin : jj;
+    if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jo) * Fout + ff] = s;
   }
 }
 
@@ -640,11 +660,17 @@ bool rowgemm_ok(int Kc, int lda, int Nc) {
 
 hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const float* B, int64_t bs_k,
                           int64_t bs_j, int64_t bs_p, int planes, int Nc, float* C, int ldc,
-                          int64_t c_plane, hipStream_t s, const float* res, int act, int pfin) {
+                          int64_t c_plane, hipStream_t s, const float* res, int act, int pfin,
+                          int apl_fin, int64_t apl_stride, int bmapK) {
   if (pfin > 0 && (planes != 1 || res || act)) return hipErrorInvalidValue;
+  if (apl_fin > 0 && (apl_fin % 16 != 0 || apl_stride % 4 != 0 || Kc < 32 || planes != 1 ||
+                      pfin > 0 || bmapK < 1))
+    return hipErrorInvalidValue;
+  const int arow_elems = apl_fin > 0 ? apl_fin : lda;
   RowGemmArgs a{A, R, Kc, lda, rowgemm_kc2(Kc), B, bs_k, bs_j, bs_p, Nc, C, ldc, c_plane,
                 res, act, pfin,
-                int(lda % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0)};
+                int(arow_elems % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0),
+                apl_fin, apl_stride, bmapK};
   const int NT = (Nc + 31) / 32;
   const size_t lds = size_t(2) * a.KC2 * NT * 32 * 4;
   const int64_t ntiles = (R + 127) / 128;
@@ -721,11 +747,12 @@ int dw_chunks(int64_t R) {
 }
 
 hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
-                           float* slab, hipStream_t s) {
+                           float* slab, hipStream_t s, int pl_fin, int64_t pl_stride, int K) {
   const int chunks = dw_chunks(R);
   const int64_t rpc = (R + chunks - 1) / chunks;
   const dim3 grid(chunks, ((FinK + 31) / 32) * ((Fout + 31) / 32));
-  hipLaunchKernelGGL(k_dw_slabs, grid, dim3(256), 0, s, basis, dy, R, FinK, Fout, rpc, slab);
+  hipLaunchKernelGGL(k_dw_slabs, grid, dim3(256), 0, s, basis, dy, R, FinK, Fout, rpc, slab,
+                     pl_fin, pl_stride, K);
   return hipGetLastError();
 }
 

@@ -9,6 +9,10 @@
   convN        out = cheb(h; W_N)
   loss         mean((labels - out)^2), dout = 2 (out - labels) / n, and the
                loss moving average (lib/graph_model.py:265-273)    cg_mse_loss_ema
+  (filters whose forward and backward both run the sample-major streaming
+  path with Fin % 16 == 0 -- the hidden layers at the humanflow shape -- keep
+  their basis in the planes layout, cg_cheb_forward_layout(CG_BASIS_PLANES):
+  each Chebyshev step writes its own plane, no rows-layout assembly pass)
   backward     cg_cheb_backward_ex per filter in reverse: ReLU mask from the
                saved outputs, the residual branch's gradient dz1 doubles as the
                buffer the sublayer-0 input gradient is ACCUMULATED into
@@ -68,8 +72,12 @@ class _ResNet:
             off += sz
         self.end = off
         self.names = [name for name, *_ in layers]
-        # activations / bases saved by the forward, gradient work buffers
-        self.basis = [torch.empty((N * M, fi * K), **f32) for _, fi, _, _ in layers]
+        # activations / bases saved by the forward, gradient work buffers; the
+        # basis layout per filter: planes where it applies, else rows
+        self.layout = ["planes" if owner.plan.basis_elems(N, fi, K, fo, "planes") else "rows"
+                       for _, fi, fo, _ in layers]
+        self.basis = [torch.empty((K, N * M, fi) if lay == "planes" else (N * M, fi * K), **f32)
+                      for (_, fi, _, _), lay in zip(layers, self.layout)]
         self.out = [torch.empty((N, M, fo), **f32) for _, _, fo, _ in layers]
         self.g = [torch.empty((N, M, F), **f32) for _ in range(3)]
 
@@ -88,18 +96,20 @@ class _ResNet:
         _, fi, fo, act = self.layers[li]
         st = o._fwd(o.plan.handle, o.N, fi, o.K, fo, x.data_ptr(), self.W[li].data_ptr(),
                     res.data_ptr() if res is not None else None, ops.ACTS[act],
-                    self.basis[li].data_ptr(), self.out[li].data_ptr(), o.ws.data_ptr(), o.ws_n, s)
-        _lib.check("cg_cheb_forward_ex", st)
+                    _lib.BASIS_LAYOUTS[self.layout[li]], self.basis[li].data_ptr(),
+                    self.out[li].data_ptr(), o.ws.data_ptr(), o.ws_n, s)
+        _lib.check("cg_cheb_forward_layout", st)
         return self.out[li]
 
     def _b(self, li, dy, dz, dx, dx_acc, s):
         o = self.o
         _, fi, fo, act = self.layers[li]
         st = o._bwd(o.plan.handle, o.N, fi, o.K, fo, dy.data_ptr(), self.out[li].data_ptr(),
-                    ops.ACTS[act], self.basis[li].data_ptr(), self.W[li].data_ptr(),
-                    dx.data_ptr() if dx is not None else None, int(dx_acc), self.dW[li].data_ptr(),
-                    dz.data_ptr() if dz is not None else None, o.ws.data_ptr(), o.ws_n, s)
-        _lib.check("cg_cheb_backward_ex", st)
+                    ops.ACTS[act], _lib.BASIS_LAYOUTS[self.layout[li]], self.basis[li].data_ptr(),
+                    self.W[li].data_ptr(), dx.data_ptr() if dx is not None else None, int(dx_acc),
+                    self.dW[li].data_ptr(), dz.data_ptr() if dz is not None else None,
+                    o.ws.data_ptr(), o.ws_n, s)
+        _lib.check("cg_cheb_backward_layout", st)
 
     def forward(self, x, s):
         h = self._f(0, x, None, s)
@@ -158,7 +168,8 @@ class _Trainer:
         self.mws = torch.empty(max(nb.value, 1), device=self.device, dtype=torch.uint8)
         self.mws_n = nb.value
         h = _lib.lib()
-        self._fwd, self._bwd, self._mse, self._adam = (h.cg_cheb_forward_ex, h.cg_cheb_backward_ex,
+        self._fwd, self._bwd, self._mse, self._adam = (h.cg_cheb_forward_layout,
+                                                       h.cg_cheb_backward_layout,
                                                        h.cg_mse_loss_ema, h.cg_adam_update)
 
     def _alloc_ws(self, nets):

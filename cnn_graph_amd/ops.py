@@ -177,9 +177,12 @@ class ChebRunner:
 
     def __init__(self, plan: ChebPlan, N: int, Fin: int, K: int, Fout: int, device,
                  basis_layout: str = "rows"):
-        """basis_layout: 'rows' ([N*M, Fin*K], lib/graph_conv.py:172) or 'orders'
+        """basis_layout: 'rows' ([N*M, Fin*K], lib/graph_conv.py:172), 'orders'
         ([N, Fin*K, Mb], one plane per order: the fast forward stores it during
-        the recurrence; Fin <= 2 fast path with fused dW only).  The basis is
+        the recurrence; Fin <= 2 fast path with fused dW only) or 'planes'
+        ([K, N*M, Fin], T_k in the layout of x: the streaming steps write their
+        own plane and skip the basis assembly; sample-major streaming path with
+        Fin % 16 == 0 only).  The basis is
         this runner's saved tensor either way.  On config B the orders layout
         makes the forward ~1.3 us faster and the backward ~1.9 us slower
         (profiles/r02_orders), so 'rows' stays the default."""
@@ -194,6 +197,11 @@ class ChebRunner:
                 raise ValueError("orders basis layout does not apply to this shape "
                                  "(needs the fast forward and the fused-dW fast backward)")
             self.basis = torch.empty((N, Fin * K, (M + 31) // 32 * 32), **f32)
+        elif basis_layout == "planes":
+            if plan.basis_elems(N, Fin, K, Fout, "planes") is None:
+                raise ValueError("planes basis layout does not apply to this shape (needs the "
+                                 "sample-major streaming path, Fin % 16 == 0, K >= 2)")
+            self.basis = torch.empty((K, N * M, Fin), **f32)
         elif basis_layout == "rows":
             self.basis = torch.empty((N * M, Fin * K), **f32)
         else:
@@ -213,6 +221,8 @@ class ChebRunner:
         """The saved basis as [N*M, Fin*K] (a copy when the layout is 'orders')."""
         if self.basis_layout == "rows":
             return self.basis
+        if self.basis_layout == "planes":  # [K][N*M][Fin] -> column fin*K + k
+            return self.basis.permute(1, 2, 0).reshape(self.N * self.plan.M, self.Fin * self.K)
         M = self.plan.M
         return self.basis[:, :, :M].permute(0, 2, 1).reshape(self.N * M, self.Fin * self.K)
 

@@ -99,9 +99,9 @@ class ChebPlan:
         return self._shape_info(N, Fin, K, Fout)[1:]
 
     def basis_elems(self, N, Fin, K, Fout, layout: str = "rows"):
-        """Floats of the basis buffer in ``layout`` ('rows' [N*M, Fin*K] or 'orders'
-        [N, Fin*K, Mb]), or None where the layout does not apply to this shape
-        (cg_cheb_basis_elems)."""
+        """Floats of the basis buffer in ``layout`` ('rows' [N*M, Fin*K], 'orders'
+        [N, Fin*K, Mb] or 'planes' [K, N*M, Fin]), or None where the layout does
+        not apply to this shape (cg_cheb_basis_elems)."""
         n = ctypes.c_int64()
         st = self._lib.cg_cheb_basis_elems(self._h, N, Fin, K, Fout, _lib.BASIS_LAYOUTS[layout],
                                            ctypes.byref(n))

@@ -153,12 +153,22 @@ int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_
  *                    after it.  Only for Fin <= 2 where the fast resident forward
  *                    AND the fused-dW fast backward apply (else CG_ERR_UNSUPPORTED),
  *                    and the backward must compute dx with dW.
+ *   CG_BASIS_PLANES  [K][N*M][Fin]: plane k is T_k in the layout of x (plane 0
+ *                    a copy of x), so each streaming Chebyshev step writes its
+ *                    own plane and the rows-layout assembly of the last step
+ *                    (a read of T_0..T_{K-2} and a write of the whole basis)
+ *                    disappears; the contraction and dW read the planes.  Only
+ *                    where forward and backward both run the sample-major
+ *                    streaming path with Fin a multiple of 16 and K >= 2 (the
+ *                    ResGNN hidden layers), else CG_ERR_UNSUPPORTED.
  * Same values either way (bit-exact basis, y and dx; dW sums its per-wave row
- * chunks in another grouping, so it agrees to fp32 rounding).
+ * chunks in another grouping, so it agrees to fp32 rounding; with the planes
+ * layout y sums its inner dimension in another order, agreeing to fp32
+ * rounding, and dW is bitwise the rows layout's).
  * cg_cheb_basis_elems: floats the basis buffer of that layout holds, or
  * CG_ERR_UNSUPPORTED where the layout does not apply.
  * ------------------------------------------------------------------------- */
-enum { CG_BASIS_ROWS = 0, CG_BASIS_ORDERS = 1 };
+enum { CG_BASIS_ROWS = 0, CG_BASIS_ORDERS = 1, CG_BASIS_PLANES = 2 };
 int cg_cheb_basis_elems(const cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                         int32_t layout, int64_t* elems);
 int cg_cheb_forward_layout(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,

@@ -1,10 +1,13 @@
-"""Orders basis layout (CG_BASIS_ORDERS, [N][Fin*K][Mb]): the fast forward
+"""Basis layouts other than the reference's rows layout.
+
+Orders basis layout (CG_BASIS_ORDERS, [N][Fin*K][Mb]): the fast forward
 stores each Chebyshev order pair during the recurrence and the fused-dW fast
 backward reads the planes back.  Bar: basis (re-laid to rows), y and dx
 BITWISE equal to the rows layout (lib/graph_conv.py:172) and the basis bitwise
 equal to the reference-generated golden basis; padding rows zero; dW (which
 sums its per-wave row chunks in another grouping) within 1e-6 normwise of the
-rows-layout dW and 1e-5 of the golden/oracle dW; Adam on top agrees."""
+rows-layout dW and 1e-5 of the golden/oracle dW; Adam on top agrees.
+Planes layout (CG_BASIS_PLANES, [K][N*M][Fin]): see the section at the end."""
 import numpy as np
 import pytest
 import scipy.sparse
@@ -145,3 +148,63 @@ def test_orders_layout_unsupported(dev):
     with pytest.raises(_lib.CGError):
         ro.backward(torch.randn((8, M, 32), device=dev), W, need_dx=False)
 
+
+
+# ---- planes layout (CG_BASIS_PLANES, [K][N*M][Fin]) ---------------------------------
+# The streaming path's layout for the ResGNN hidden layers: each Chebyshev step
+# writes T_k as its own plane (plane 0 = x), the rows-layout assembly pass
+# disappears, the row GEMM and the dW slabs read the planes.  Bar: basis
+# (re-laid to rows) and dx BITWISE equal to the rows layout, dW bitwise too
+# (each dW element sums the same rows in the same order), y within 1e-5 of the
+# float64 oracle (its inner dimension is summed in another order).
+@pytest.mark.parametrize("N,Fin,K,Fout", [(4, 32, 6, 32), (5, 32, 20, 32), (3, 16, 4, 40),
+                                          (2, 64, 3, 64)])
+def test_planes_layout_vs_rows(dev, N, Fin, K, Fout):
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden("golden_B.npz"))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    plan = ChebPlan(Lt, device=0, path="stream")
+    rng = np.random.default_rng(N * 1000 + Fin + K)
+    x = rng.standard_normal((N, M, Fin)).astype(np.float32)
+    W = (rng.standard_normal((Fin * K, Fout)) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((N, M, Fout)).astype(np.float32)
+    res = rng.standard_normal((N, M, Fout)).astype(np.float32)
+    rr = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
+    rp = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="planes")
+    assert tuple(rp.basis.shape) == (K, N * M, Fin)
+    xt, Wt, dyt = _t(x, dev), _t(W, dev), _t(dy, dev)
+    for r in (rr, rp):
+        r.forward(xt, Wt)
+        r.backward(dyt, Wt)
+    torch.cuda.synchronize()
+    assert torch.equal(rp.basis_rows(), rr.basis), "planes basis differs from the rows basis"
+    assert torch.equal(rp.dx, rr.dx)
+    assert torch.equal(rp.dW, rr.dW)
+    b64 = rr.basis.cpu().numpy().astype(np.float64)
+    y64 = (b64 @ W.astype(np.float64)).reshape(N, M, Fout)
+    assert O.normwise_err(rp.y.cpu().numpy(), y64) < 1e-5
+    # the residual + ReLU epilogue of the planes row GEMM (cg_cheb_forward_layout)
+    from cnn_graph_amd import _lib
+    y2 = torch.empty((N, M, Fout), device=dev)
+    _lib.check("cg_cheb_forward_layout", _lib.lib().cg_cheb_forward_layout(
+        plan.handle, N, Fin, K, Fout, xt.data_ptr(), Wt.data_ptr(), _t(res, dev).data_ptr(),
+        _lib.CG_ACT_RELU, _lib.CG_BASIS_PLANES, rp.basis.data_ptr(), y2.data_ptr(),
+        rp.ws.data_ptr(), rp.fwd_bytes, torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert O.normwise_err(y2.cpu().numpy(), np.maximum(y64 + res, 0)) < 1e-5
+
+
+def test_planes_layout_unsupported(dev):
+    """Resident shapes, Fin not a multiple of 16 and K = 1 refuse the planes layout."""
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden("golden_B.npz"))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    auto = ChebPlan(Lt, device=0, path="auto")
+    stream = ChebPlan(Lt, device=0, path="stream")
+    assert auto.basis_elems(8, 1, 25, 32, "planes") is None   # fast resident path
+    assert stream.basis_elems(8, 8, 5, 32, "planes") is None  # Fin % 16 != 0
+    assert stream.basis_elems(8, 32, 1, 32, "planes") is None  # K = 1
+    assert stream.basis_elems(8, 32, 5, 32, "planes") == 8 * M * 32 * 5
