@@ -126,7 +126,8 @@ struct Vec<4> {
 // sum_{j in row r, CSR order} val[j] * S[col[j]*Fin + f0 .. +VEC), sequential
 // from +0 with one rounding per product and per add (the order of scipy
 // csr_matvecs / TF's SparseTensorDenseMatMul).  Four entries' loads are issued
-// before their (in-order) accumulation.
+// before their (in-order) accumulation (eight were measured 1-2 % slower on
+// configs R and C2, profiles/r02_planes/gather8_ab).
 template <int VEC>
 __device__ __forceinline__ typename Vec<VEC>::T row_spmm(const int* __restrict__ col,
                                                          const float* __restrict__ val, int j0,

@@ -10,7 +10,7 @@
 fwd / bwd are HIP-event timings (torch's current stream, where every C-ABI
 call is enqueued) of one chebyshev5 forward and backward (dx + dW), median of
 rounds; alg_GBps uses SURVEY.md §8d's algorithmic bytes.
-Usage: python scripts/bench_configs.py [C1 C2 D E] [--d-batch N]
+Usage: python scripts/bench_configs.py [C1 C2 D E R] [--d-batch N] [--layout rows|planes]
 """
 from __future__ import annotations
 
@@ -49,7 +49,7 @@ def alg_bytes(M, nnz, B, K):
     return (K - 1) * csr + 4 * M * B * (2 + 3 * (K - 2)), (K - 1) * csr + 4 * M * B * (3 + 5 * (K - 2))
 
 
-def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto"):
+def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="rows"):
     M = Lt.shape[0]
     plan = ChebPlan(Lt, device=0, variant=variant)
     g = torch.Generator(device=dev)
@@ -57,7 +57,9 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto"):
     x = torch.rand((N, M, Fin), device=dev, generator=g)
     W = torch.randn((Fin * K, Fout), device=dev, generator=g) * 0.1
     dy = torch.randn((N, M, Fout), device=dev, generator=g)
-    r = ops.ChebRunner(plan, N, Fin, K, Fout, dev)
+    if layout != "rows" and plan.basis_elems(N, Fin, K, Fout, layout) is None:
+        return None  # the layout does not apply to this shape
+    r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=layout)
     r.forward(x, W)
     r.backward(dy, W)
     torch.cuda.synchronize()
@@ -66,7 +68,8 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto"):
     b = ev_ms(lambda: r.backward(dy, W), reps)
     bf, bb = alg_bytes(M, plan.nnz, N * Fin, K)
     return {"config": name, "M": M, "nnz": plan.nnz, "N": N, "Fin": Fin, "K": K, "Fout": Fout,
-            "path": r.path, "variant": variant, "fwd_ms": round(f, 4), "bwd_ms": round(b, 4),
+            "path": r.path, "variant": variant, "basis_layout": layout,
+            "fwd_ms": round(f, 4), "bwd_ms": round(b, 4),
             "samples_per_s": round(N / ((f + b) * 1e-3), 1),
             "fwd_alg_GBps": round(bf / (f * 1e-3) / 1e9, 1),
             "bwd_alg_GBps": round(bb / (b * 1e-3) / 1e9, 1)}
@@ -133,6 +136,8 @@ def main():
     ap.add_argument("configs", nargs="*", default=["C1", "C2", "D", "E"])
     ap.add_argument("--d-batch", type=int, default=32)
     ap.add_argument("--variant", default="auto", help="plan variant (auto / narrow / ...)")
+    ap.add_argument("--layout", default="rows", choices=["rows", "planes"],
+                    help="basis layout of the C1/C2/D filters (planes: where it applies)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -143,11 +148,11 @@ def main():
                 M = int(z["M"])
                 Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
             Fin = 1 if name == "C1" else 32
-            out = filter_config(name, Lt, 128, Fin, 5, 32, dev, args.variant)
+            out = filter_config(name, Lt, 128, Fin, 5, 32, dev, args.variant, args.layout)
         elif name == "D":
             import synth_graphs
             Lt = rescale_L(synth_graphs.config_d_laplacian(), 2)
-            out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev, args.variant)
+            out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev, args.variant, args.layout)
         elif name == "E":
             out = lstm_config(dev)
         elif name == "E_unfused":
@@ -156,7 +161,8 @@ def main():
             out = resgnn_config(dev)
         else:
             raise SystemExit(f"unknown config {name}")
-        print(json.dumps(out), flush=True)
+        if out is not None:
+            print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
