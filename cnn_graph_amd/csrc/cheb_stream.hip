@@ -293,7 +293,10 @@ struct RowGemmArgs {
   int bmapK;
 };
 
-template <int NT>
+// PF: the A-chunk prefetch variant (its register ring costs occupancy, so the
+// host picks it only for >= 3 full chunks per half: measured D's y GEMM
+// -12 %, while the single-chunk dBasis GEMMs of C2 / R lost 6 % with it)
+template <int NT, bool PF>
 __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
   extern __shared__ float Bs[];  // [2*KC2][NT*32]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -330,24 +333,7 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
-    for (int c0 = 0; c0 < a.KC2; c0 += 16) {
-      float av[16];
-      const int k0 = kbeg + c0;
-      const int nq = (a.KC2 - c0 < 16) ? a.KC2 - c0 : 16;  // (small Kc: no padded MFMAs)
-      if (a.vecA && nq == 16 && k0 + 16 <= a.Kc) {
-        const float* ap = aptr(k0);  // 16 contiguous floats (host: apl_fin % 16 == 0)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
-          av[4 * q] = v.x;
-          av[4 * q + 1] = v.y;
-          av[4 * q + 2] = v.z;
-          av[4 * q + 3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) av[q] = (q < nq && k0 + q < a.Kc) ? *aptr(k0 + q) : 0.f;
-      }
+    auto mm = [&](const float (&av)[16], int c0, int nq) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         if (q < nq) {
@@ -356,6 +342,59 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
           for (int t = 0; t < NT; ++t)
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], brow[t * 32], acc[t], 0, 0, 0);
         }
+      }
+    };
+    if constexpr (PF) {
+      // every chunk is 16 contiguous in-range floats: loaded two chunks ahead
+      // of their MFMAs through a 3-buffer register ring (one wave per SIMD
+      // when B fills the LDS, so nothing else hides a chunk's HBM latency)
+      auto ld = [&](float (&av)[16], int c0) {
+        const float* ap = aptr(kbeg + c0);  // (host: apl_fin % 16 == 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
+          av[4 * q] = v.x;
+          av[4 * q + 1] = v.y;
+          av[4 * q + 2] = v.z;
+          av[4 * q + 3] = v.w;
+        }
+      };
+      const int nch = a.KC2 / 16;
+      float b0[16], b1[16], b2[16];
+      ld(b0, 0);
+      if (nch > 1) ld(b1, 16);
+      for (int ci = 0; ci < nch; ci += 3) {
+        if (ci + 2 < nch) ld(b2, (ci + 2) * 16);
+        mm(b0, ci * 16, 16);
+        if (ci + 1 < nch) {
+          if (ci + 3 < nch) ld(b0, (ci + 3) * 16);
+          mm(b1, (ci + 1) * 16, 16);
+        }
+        if (ci + 2 < nch) {
+          if (ci + 4 < nch) ld(b1, (ci + 4) * 16);
+          mm(b2, (ci + 2) * 16, 16);
+        }
+      }
+    } else {
+      for (int c0 = 0; c0 < a.KC2; c0 += 16) {
+        float av[16];
+        const int k0 = kbeg + c0;
+        const int nq = (a.KC2 - c0 < 16) ? a.KC2 - c0 : 16;  // (small Kc: no padded MFMAs)
+        if (a.vecA && nq == 16 && k0 + 16 <= a.Kc) {
+          const float* ap = aptr(k0);  // 16 contiguous floats (host: apl_fin % 16 == 0)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = *reinterpret_cast<const float4*>(ap + 4 * q);
+            av[4 * q] = v.x;
+            av[4 * q + 1] = v.y;
+            av[4 * q + 2] = v.z;
+            av[4 * q + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) av[q] = (q < nq && k0 + q < a.Kc) ? *aptr(k0 + q) : 0.f;
+        }
+        mm(av, c0, nq);
       }
     }
 #pragma unroll
@@ -681,30 +720,44 @@ hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const floa
     static hipError_t attr[8] = {};
     static bool set = false;
     if (!set) {
-      const void* ks[8] = {reinterpret_cast<const void*>(&k_rowgemm<1>),
-                           reinterpret_cast<const void*>(&k_rowgemm<2>),
-                           reinterpret_cast<const void*>(&k_rowgemm<3>),
-                           reinterpret_cast<const void*>(&k_rowgemm<4>),
-                           reinterpret_cast<const void*>(&k_rowgemm<5>),
-                           reinterpret_cast<const void*>(&k_rowgemm<6>),
-                           reinterpret_cast<const void*>(&k_rowgemm<7>),
-                           reinterpret_cast<const void*>(&k_rowgemm<8>)};
-      for (int q = 0; q < 8; ++q)
+      const void* ks[16] = {reinterpret_cast<const void*>(&k_rowgemm<1, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<2, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<3, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<4, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<5, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<6, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<7, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<8, false>),
+                            reinterpret_cast<const void*>(&k_rowgemm<1, true>),
+                            reinterpret_cast<const void*>(&k_rowgemm<2, true>),
+                            reinterpret_cast<const void*>(&k_rowgemm<3, true>),
+                            reinterpret_cast<const void*>(&k_rowgemm<4, true>),
+                            reinterpret_cast<const void*>(&k_rowgemm<5, true>),
+                            reinterpret_cast<const void*>(&k_rowgemm<6, true>),
+                            reinterpret_cast<const void*>(&k_rowgemm<7, true>),
+                            reinterpret_cast<const void*>(&k_rowgemm<8, true>)};
+      for (int q = 0; q < 8; ++q) {
         attr[q] = hipFuncSetAttribute(ks[q], hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        if (attr[q] == hipSuccess)
+          attr[q] = hipFuncSetAttribute(ks[q + 8], hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        kLdsBytes);
+      }
       set = true;
     }
     if (attr[(NT < 8 ? NT : 8) - 1] != hipSuccess) return attr[(NT < 8 ? NT : 8) - 1];
   }
-  switch (NT) {
-    case 1: hipLaunchKernelGGL(k_rowgemm<1>, grid, block, lds, s, a); break;
-    case 2: hipLaunchKernelGGL(k_rowgemm<2>, grid, block, lds, s, a); break;
-    case 3: hipLaunchKernelGGL(k_rowgemm<3>, grid, block, lds, s, a); break;
-    case 4: hipLaunchKernelGGL(k_rowgemm<4>, grid, block, lds, s, a); break;
-    case 5: hipLaunchKernelGGL(k_rowgemm<5>, grid, block, lds, s, a); break;
-    case 6: hipLaunchKernelGGL(k_rowgemm<6>, grid, block, lds, s, a); break;
-    case 7: hipLaunchKernelGGL(k_rowgemm<7>, grid, block, lds, s, a); break;
-    default: hipLaunchKernelGGL(k_rowgemm<8>, grid, block, lds, s, a); break;
+  // every chunk 16 contiguous in-range floats, at least 3 of them per half
+  const bool pf = a.vecA && a.KC2 % 16 == 0 && 2 * a.KC2 <= Kc && a.KC2 / 16 >= 3;
+#define CG_RG(nt)                                                                 \
+  case nt:                                                                        \
+    if (pf) hipLaunchKernelGGL((k_rowgemm<nt, true>), grid, block, lds, s, a);    \
+    else hipLaunchKernelGGL((k_rowgemm<nt, false>), grid, block, lds, s, a);      \
+    break;
+  switch (NT < 8 ? NT : 8) {
+    CG_RG(1) CG_RG(2) CG_RG(3) CG_RG(4) CG_RG(5) CG_RG(6) CG_RG(7)
+    default: CG_RG(8)
   }
+#undef CG_RG
   return hipGetLastError();
 }
 
