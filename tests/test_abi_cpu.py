@@ -146,3 +146,18 @@ def test_forward_adam_validates(built_lib):
     assert h.cg_cheb_forward_adam(None, 1, 1, 2, 1, None, p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 1,
                                   1.0, q, r, r, 0, None, y, None, 0, None) == _lib.CG_ERR_ARG
     assert "distinct" in h.cg_last_error().decode()
+
+
+def test_header_enums_match_the_binding(built_lib):
+    """The ctypes binding's constants are the header's (basis layouts, paths,
+    variants, activations, status codes)."""
+    import re
+    from cnn_graph_amd import _lib
+    text = open(_lib.HEADER_PATH).read()
+    consts = {m.group(1): int(m.group(2)) for m in re.finditer(r"\b(CG_[A-Z_]+)\s*=\s*(-?\d+)", text)}
+    for name in ("CG_BASIS_ROWS", "CG_BASIS_ORDERS", "CG_BASIS_PLANES", "CG_PATH_AUTO",
+                 "CG_PATH_RESIDENT", "CG_PATH_STREAM", "CG_ACT_NONE", "CG_ACT_RELU"):
+        assert name in consts, name
+        assert getattr(_lib, name) == consts[name], name
+    assert _lib.BASIS_LAYOUTS == {"rows": consts["CG_BASIS_ROWS"], "orders": consts["CG_BASIS_ORDERS"],
+                                  "planes": consts["CG_BASIS_PLANES"]}
