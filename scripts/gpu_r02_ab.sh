@@ -1,7 +1,7 @@
-# r02: row GEMM A chunks prefetched two ahead (k_rowgemm), A/B vs
+# r02: streaming SpMM rows: next batch of col/val issued behind the gathers (row_spmm), A/B vs
 # the library before it (scripts/_debug/libcheb_planes.so) on configs R, C2, D
 set -o pipefail
-O=gpurun_out/t9
+O=gpurun_out/t10
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_large.py tests/test_gpu_basis_layout.py tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && echo PYTEST_OK &&
 for i in 1 2; do
