@@ -60,12 +60,21 @@ def _check_out(name, t, shape):
 ACTS = {"none": _lib.CG_ACT_NONE, "relu": _lib.CG_ACT_RELU}
 
 
+def basis_layout_for(plan: ChebPlan, N: int, Fin: int, K: int, Fout: int) -> str:
+    """The layout a caller that keeps the basis to itself (the autograd
+    functions below) should use: 'planes' where it applies (sample-major
+    streaming path, Fin % 16 == 0: no basis-assembly pass), else 'rows'."""
+    return "planes" if plan.basis_elems(N, Fin, K, Fout, "planes") else "rows"
+
+
 def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int,
                  want_basis: bool = True, out_basis: torch.Tensor | None = None,
                  out_y: torch.Tensor | None = None, residual: torch.Tensor | None = None,
-                 act: str = "none"):
+                 act: str = "none", layout: str = "rows"):
     """Basis (N*M, Fin*K) and y = act(basis @ W + residual) (N, M, Fout).
-    W None -> basis only.  out_basis / out_y: pre-allocated contiguous outputs."""
+    W None -> basis only.  out_basis / out_y: pre-allocated contiguous outputs.
+    layout: the basis layout ('rows' = lib/graph_conv.py:172; 'planes' =
+    [K, N*M, Fin], see ChebRunner); pass the same one to the backward."""
     _check_dev("x", x)
     x = x.contiguous()
     N, M, Fin = x.shape
@@ -84,7 +93,8 @@ def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int
     need_basis = want_basis or W is None or plan.query_path(N, Fin, K, Fout) == "stream"
     basis = y = None
     if need_basis:
-        basis = out_basis if out_basis is not None else torch.empty((N * M, Fin * K), device=dev,
+        shape = (K, N * M, Fin) if layout == "planes" else (N * M, Fin * K)
+        basis = out_basis if out_basis is not None else torch.empty(shape, device=dev,
                                                                     dtype=torch.float32)
         _check_out("out_basis", basis, (N * M, Fin * K))
     if W is not None:
@@ -97,14 +107,14 @@ def cheb_forward(plan: ChebPlan, x: torch.Tensor, W: torch.Tensor | None, K: int
             raise ValueError(f"residual must be [N, M, Fout] = [{N}, {M}, {Fout}]")
     fwd_ws, _ = plan.workspace_bytes(N, Fin, K, Fout)
     ws, s = _plan_ws(plan, fwd_ws, x)
-    _lib.call("cg_cheb_forward_ex", plan.handle, N, Fin, K, Fout, _p(x), _p(W), _p(residual),
-              ACTS[act], _p(basis), _p(y), _p(ws), fwd_ws, s)
+    _lib.call("cg_cheb_forward_layout", plan.handle, N, Fin, K, Fout, _p(x), _p(W), _p(residual),
+              ACTS[act], _lib.BASIS_LAYOUTS[layout], _p(basis), _p(y), _p(ws), fwd_ws, s)
     return basis, y
 
 
 def cheb_backward(plan: ChebPlan, dy: torch.Tensor, basis: torch.Tensor, W: torch.Tensor, K: int,
-                  need_dx: bool = True, need_dW: bool = True):
-    """(dx [N,M,Fin] or None, dW [Fin*K, Fout] or None)."""
+                  need_dx: bool = True, need_dW: bool = True, layout: str = "rows"):
+    """(dx [N,M,Fin] or None, dW [Fin*K, Fout] or None); layout: the forward's."""
     _check_dev("dy", dy)
     dy = dy.contiguous()
     N, M, Fout = dy.shape
@@ -115,14 +125,16 @@ def cheb_backward(plan: ChebPlan, dy: torch.Tensor, basis: torch.Tensor, W: torc
     dW = torch.empty((FinK, Fout), device=dev, dtype=torch.float32) if need_dW else None
     _, bwd_ws = plan.workspace_bytes(N, Fin, K, Fout)
     ws, s = _plan_ws(plan, bwd_ws, dy)
-    _lib.call("cg_cheb_backward", plan.handle, N, Fin, K, Fout, _p(dy), _p(basis), _p(W.contiguous()),
-              _p(dx), _p(dW), _p(ws), bwd_ws, s)
+    _lib.call("cg_cheb_backward_layout", plan.handle, N, Fin, K, Fout, _p(dy), None,
+              _lib.CG_ACT_NONE, _lib.BASIS_LAYOUTS[layout], _p(basis), _p(W.contiguous()), _p(dx),
+              0, _p(dW), None, _p(ws), bwd_ws, s)
     return dx, dW
 
 
 def cheb_backward_ex(plan: ChebPlan, dy: torch.Tensor, y: torch.Tensor | None, act: str,
                      basis: torch.Tensor, W: torch.Tensor, K: int, dx: torch.Tensor | None = None,
-                     dx_accumulate: bool = False, need_dx: bool = True, need_dW: bool = True):
+                     dx_accumulate: bool = False, need_dx: bool = True, need_dW: bool = True,
+                     layout: str = "rows"):
     """Backward through y = act(basis W + residual): returns (dx, dW, dz) where
     dz = dy * act'(y) is also the gradient of the residual input.  With
     dx_accumulate the input gradient is added into the given ``dx``."""
@@ -142,9 +154,9 @@ def cheb_backward_ex(plan: ChebPlan, dy: torch.Tensor, y: torch.Tensor | None, a
     dz = torch.empty((N, M, Fout), device=dev, dtype=torch.float32)
     _, bwd_ws = plan.workspace_bytes(N, Fin, K, Fout)
     ws, s = _plan_ws(plan, bwd_ws, dy)
-    _lib.call("cg_cheb_backward_ex", plan.handle, N, Fin, K, Fout, _p(dy), _p(y), ACTS[act],
-              _p(basis), _p(W.contiguous()), _p(dx if need_dx else None), int(dx_accumulate),
-              _p(dW), _p(dz), _p(ws), bwd_ws, s)
+    _lib.call("cg_cheb_backward_layout", plan.handle, N, Fin, K, Fout, _p(dy), _p(y), ACTS[act],
+              _lib.BASIS_LAYOUTS[layout], _p(basis), _p(W.contiguous()),
+              _p(dx if need_dx else None), int(dx_accumulate), _p(dW), _p(dz), _p(ws), bwd_ws, s)
     return (dx if need_dx else None), dW, dz
 
 
@@ -290,15 +302,18 @@ class ChebConv(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, plan: ChebPlan, K: int):
-        basis, y = cheb_forward(plan, x, W, K, want_basis=True)
+        # the saved basis is internal: the planes layout where it applies
+        lay = basis_layout_for(plan, x.shape[0], x.shape[2], K, W.shape[1])
+        basis, y = cheb_forward(plan, x, W, K, want_basis=True, layout=lay)
         ctx.save_for_backward(basis, W)
-        ctx.plan, ctx.K = plan, K
+        ctx.plan, ctx.K, ctx.layout = plan, K, lay
         return y
 
     @staticmethod
     def backward(ctx, dy):
         basis, W = ctx.saved_tensors
-        dx, dW = cheb_backward(ctx.plan, dy, basis, W, ctx.K, need_dx=ctx.needs_input_grad[0])
+        dx, dW = cheb_backward(ctx.plan, dy, basis, W, ctx.K, need_dx=ctx.needs_input_grad[0],
+                               layout=ctx.layout)
         return dx, dW, None, None
 
 
@@ -308,16 +323,19 @@ class ChebConvAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, W, residual, plan: ChebPlan, K: int, act: str):
-        basis, y = cheb_forward(plan, x, W, K, want_basis=True, residual=residual, act=act)
+        lay = basis_layout_for(plan, x.shape[0], x.shape[2], K, W.shape[1])
+        basis, y = cheb_forward(plan, x, W, K, want_basis=True, residual=residual, act=act,
+                                layout=lay)
         ctx.save_for_backward(basis, W, y)
         ctx.plan, ctx.K, ctx.act, ctx.has_res = plan, K, act, residual is not None
+        ctx.layout = lay
         return y
 
     @staticmethod
     def backward(ctx, dy):
         basis, W, y = ctx.saved_tensors
         dx, dW, dz = cheb_backward_ex(ctx.plan, dy, y, ctx.act, basis, W, ctx.K,
-                                      need_dx=ctx.needs_input_grad[0])
+                                      need_dx=ctx.needs_input_grad[0], layout=ctx.layout)
         return dx, dW, (dz if ctx.has_res else None), None, None, None
 
 

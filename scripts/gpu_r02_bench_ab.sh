@@ -1,6 +1,6 @@
 # r02: headline bench A/B, current library vs scripts/_debug/libcheb_planes.so
 set -o pipefail
-O=gpurun_out/t11
+O=gpurun_out/t12
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_basis_layout.py tests/test_gpu_fused_adam.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && echo PYTEST_OK &&
 for i in 1 2 3; do

@@ -208,3 +208,29 @@ def test_planes_layout_unsupported(dev):
     assert stream.basis_elems(8, 8, 5, 32, "planes") is None  # Fin % 16 != 0
     assert stream.basis_elems(8, 32, 1, 32, "planes") is None  # K = 1
     assert stream.basis_elems(8, 32, 5, 32, "planes") == 8 * M * 32 * 5
+
+
+def test_autograd_uses_planes_with_rows_gradients(dev):
+    """ops.cheb_conv (the GraphConv.chebyshev5 autograd path) keeps its saved
+    basis in the planes layout on a Fin = 32 streaming shape: its dx and dW are
+    bitwise the explicit rows-layout backward's, y within 1e-5 of float64."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden("golden_B.npz"))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    plan = ChebPlan(Lt, device=0, path="stream")
+    N, Fin, K, Fout = 3, 32, 5, 32
+    assert ops.basis_layout_for(plan, N, Fin, K, Fout) == "planes"
+    rng = np.random.default_rng(9)
+    x = _t(rng.standard_normal((N, M, Fin)), dev).requires_grad_(True)
+    W = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev).requires_grad_(True)
+    dy = _t(rng.standard_normal((N, M, Fout)), dev)
+    y = ops.cheb_conv(x, W, plan, K)
+    y.backward(dy)
+    basis, y_rows = ops.cheb_forward(plan, x.detach(), W.detach(), K)
+    dx_r, dW_r = ops.cheb_backward(plan, dy, basis, W.detach(), K)
+    torch.cuda.synchronize()
+    assert torch.equal(x.grad, dx_r) and torch.equal(W.grad, dW_r)
+    y64 = (basis.cpu().numpy().astype(np.float64) @ W.detach().cpu().numpy().astype(np.float64))
+    assert O.normwise_err(y.detach().cpu().numpy().reshape(N * M, Fout), y64) < 1e-5
