@@ -1,6 +1,5 @@
-# r02: the whole GPU suite on the current tree
+# r02: the planes-layout GPU tests on the current tree
 set -o pipefail
-O=gpurun_out/t12
+O=gpurun_out/t13
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && echo PYTEST_OK &&
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 && echo SMOKE_OK
+timeout -k 10 300 python -u -m pytest tests/test_gpu_basis_layout.py -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && echo PYTEST_OK

@@ -234,3 +234,51 @@ def test_autograd_uses_planes_with_rows_gradients(dev):
     assert torch.equal(x.grad, dx_r) and torch.equal(W.grad, dW_r)
     y64 = (basis.cpu().numpy().astype(np.float64) @ W.detach().cpu().numpy().astype(np.float64))
     assert O.normwise_err(y.detach().cpu().numpy().reshape(N * M, Fout), y64) < 1e-5
+
+
+def test_planes_layout_skewed_graph(dev):
+    """Planes vs rows on a hub-and-spoke graph whose row lengths are skewed
+    enough for the degree-sorted row order (max row > 2 * mean + 8): the
+    steps visit rows in that order and write their planes in natural order."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    rng = np.random.default_rng(5)
+    M, hubs = 1500, 6
+    rows, cols = [], []
+    for v in range(M):                       # a ring
+        rows += [v, (v + 1) % M]
+        cols += [(v + 1) % M, v]
+    for hbv in range(hubs):                  # hubs linked to ~150 random vertices each
+        nb = rng.choice(np.arange(hubs, M), size=150, replace=False)
+        rows += [hbv] * len(nb) + list(nb)
+        cols += list(nb) + [hbv] * len(nb)
+    A = scipy.sparse.csr_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(M, M))
+    A.sum_duplicates()
+    A.data[:] = 1.0
+    d = np.asarray(A.sum(axis=1)).ravel()
+    Dm = scipy.sparse.diags((1.0 / np.sqrt(d)).astype(np.float32))
+    Lt = (-(Dm @ A @ Dm)).astype(np.float32).tocsr()   # L~ = L - I for lmax = 2
+    Lt.sort_indices()
+    lens = np.diff(Lt.indptr)
+    assert lens.max() > 2 * (Lt.nnz // M) + 8, "graph not skewed enough for the sorted row order"
+    plan = ChebPlan(Lt, device=0, path="stream")
+    N, Fin, K, Fout = 2, 16, 4, 16
+    x = _t(rng.standard_normal((N, M, Fin)), dev)
+    W = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
+    dy = _t(rng.standard_normal((N, M, Fout)), dev)
+    rr = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
+    rp = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="planes")
+    for r in (rr, rp):
+        r.forward(x, W)
+        r.backward(dy, W)
+    torch.cuda.synchronize()
+    assert torch.equal(rp.basis_rows(), rr.basis)
+    assert torch.equal(rp.dx, rr.dx) and torch.equal(rp.dW, rr.dW)
+    assert O.normwise_err(rp.y.cpu().numpy(), rr.y.cpu().numpy().astype(np.float64)) < 1e-5
+    # and the basis against the float64 recurrence of the oracle
+    xb = x.cpu().numpy().astype(np.float64)
+    T = [xb, np.stack([Lt @ xb[n] for n in range(N)])]
+    for _ in range(2, K):
+        T.append(np.stack([2 * (Lt @ T[-1][n]) for n in range(N)]) - T[-2])
+    ref = np.stack(T, axis=-1).reshape(N * M, Fin * K)  # column fin*K + k
+    assert O.normwise_err(rr.basis.cpu().numpy(), ref) < 1e-5
