@@ -257,10 +257,15 @@ def main():
     scale = ctypes.c_float(1.0 / world)
     exchange = world > 1 or args.force_allreduce
     comm = None
+    rccl_nranks = None
     if exchange and args.allreduce == "rccl":
         comm = cdist.RcclComm(local)
         ar_fn = _lib.lib().cg_allreduce_sum_f32
         ar_args = (comm.handle, runner.dW.data_ptr(), runner.dW.numel(), stream)
+        # proof that the timed exchange spans every rank (ncclCommCount)
+        rccl_nranks = comm.nranks()
+        if rccl_nranks != world:
+            sys.exit(f"bench.py: RCCL communicator spans {rccl_nranks} ranks, expected {world}")
 
     # No exchange step (one GPU): the Adam update rides on the dW reduction
     # (cg_cheb_backward_adam) instead of a separate launch.  With an exchange
@@ -303,24 +308,58 @@ def main():
             if st:
                 _lib.check("cg_adam_update", st)
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    def check_comm():
+        """After a failed step: poll RCCL's asynchronous error
+        and abort the communicator so blocked ranks return."""
+        if comm is not None:
+            st = comm.async_error(abort=True)
+            if st:
+                sys.exit(f"bench.py: RCCL asynchronous error {st} on rank {rank}")
+
+    try:
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    except Exception:
+        check_comm()
+        raise
+    check_comm()
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+
+    # per-step distribution (SURVEY.md §8d asks for the median step): a second
+    # pass of the same steps with a HIP event between consecutive steps on
+    # the launch stream (after the contract's timed region, which stays
+    # event-free); max over ranks of each rank's median
+    nstep = max(50, min(args.steps, 400))
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(nstep + 1)]
+    if world > 1:
+        dist.barrier()
+    evs[0].record()
+    for i in range(nstep):
+        step(args.warmup + args.steps + i)
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    per_step = np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(nstep)])
+    med_ms = float(np.median(per_step))
+    p90_ms = float(np.percentile(per_step, 90))
+    if world > 1:
+        tt = torch.tensor([med_ms, p90_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        med_ms, p90_ms = (float(v) for v in tt.tolist())
 
     # per-kernel timing (after the timed region): forward = one kernel;
     # backward = the recurrence kernel + the tiny fixed-order dW slab reduce
@@ -352,6 +391,9 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "step_ms_median": round(med_ms, 4),
+        "step_ms_p90": round(p90_ms, 4),
+        "samples_per_s_at_median": round(N_global / (med_ms * 1e-3), 1),
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
@@ -364,6 +406,7 @@ def main():
                    "Fin": Fin, "Fout": Fout, "path": path, "basis_layout": runner.basis_layout,
                    "parallelism": f"dp{world}",
                    "allreduce": (args.allreduce if exchange else None),
+                   "rccl_nranks": rccl_nranks,
                    "adam": ("fused into the dW reduction (cg_cheb_backward_adam)" if fuse_adam
                             else "applied by the next step's forward (cg_cheb_forward_adam)"
                             if fwd_adam else "cg_adam_update")},

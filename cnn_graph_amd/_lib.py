@@ -114,6 +114,8 @@ _SIGNATURES = {
     "cg_comm_init": ([ctypes.POINTER(_vp), _c_int, _c_int, ctypes.c_char_p, _c_int], _c_int),
     "cg_allreduce_sum_f32": ([_vp, _vp, _c_sz, _vp], _c_int),
     "cg_comm_destroy": ([_vp], _c_int),
+    "cg_comm_count": ([_vp, ctypes.POINTER(_c_int)], _c_int),
+    "cg_comm_async_error": ([_vp, ctypes.POINTER(_c_int), _c_int], _c_int),
     # host-side coarsening: numpy arrays passed by pointer
     "cg_graclus_match_f32": ([_c_i64, _vp, _vp, _vp, _c_i32, _vp, _vp, _vp,
                               ctypes.POINTER(_c_i32)], _c_int),

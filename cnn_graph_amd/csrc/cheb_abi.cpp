@@ -1389,6 +1389,11 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
                                     "(M=%d H=%d K=%d)", plan->M, H, K);
   if (planes && K > 1 && plane_stride < int64_t(N) * plan->M * H)
     return fail(CG_ERR_ARG, "lstm_hconv_step: plane stride %lld < N*M*H", (long long)plane_stride);
+  // the kernel moves h_prev and the planes as float4
+  if ((reinterpret_cast<uintptr_t>(h_prev) & 15) || (planes && (reinterpret_cast<uintptr_t>(planes) & 15)) ||
+      (planes && K > 1 && (plane_stride & 3)))
+    return fail(CG_ERR_ARG, "lstm_hconv_step: h_prev / planes must be 16-byte aligned and the "
+                            "plane stride a multiple of 4 floats");
   const void* outs[] = {c_out, h_out, act, planes};
   const void* ins[] = {h_prev, c_prev, gx};
   for (const void* o : outs)

@@ -401,7 +401,8 @@ __global__ __launch_bounds__(256) void k_wide_dypass(const float* __restrict__ d
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int n = n0 + 2 * u + h;
-      bv[u] = (li < FinK && n < N) ? basis[(int64_t(n) * M + m) * FinK + li] : 0.f;
+      // basis == NULL: a dx-only call (no dW), the dW MFMAs run on zeros
+      bv[u] = (basis && li < FinK && n < N) ? basis[(int64_t(n) * M + m) * FinK + li] : 0.f;
     }
     // the dy tile into LDS, [row][f]
 #pragma unroll
@@ -484,7 +485,7 @@ __device__ __forceinline__ void dypass_load(const float* __restrict__ dy,
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = 4 * h + q;
-    t.b[q] = (nv && j < FinK) ? basis[(int64_t(ni) * M + m) * FinK + j] : 0.f;
+    t.b[q] = (basis && nv && j < FinK) ? basis[(int64_t(ni) * M + m) * FinK + j] : 0.f;
   }
 }
 

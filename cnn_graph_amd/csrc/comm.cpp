@@ -72,6 +72,31 @@ int cg_allreduce_sum_f32(cg_comm* comm, float* buf, size_t count, void* stream) 
   return cg_internal_set_error(CG_OK, "");
 }
 
+int cg_comm_count(const cg_comm* comm, int* nranks) {
+  if (!comm || !comm->comm || !nranks) return cg_internal_set_error(CG_ERR_ARG, "comm_count: bad arguments");
+  ncclResult_t r = ncclCommCount(comm->comm, nranks);
+  if (r != ncclSuccess) return comm_fail("ncclCommCount", r);
+  return cg_internal_set_error(CG_OK, "");
+}
+
+int cg_comm_async_error(cg_comm* comm, int* async_status, int abort_on_error) {
+  if (!comm || !comm->comm || !async_status)
+    return cg_internal_set_error(CG_ERR_ARG, "comm_async_error: bad arguments");
+  ncclResult_t async = ncclSuccess;
+  ncclResult_t r = ncclCommGetAsyncError(comm->comm, &async);
+  if (r != ncclSuccess) return comm_fail("ncclCommGetAsyncError", r);
+  *async_status = int(async);
+  if (async == ncclSuccess || async == ncclInProgress) {
+    *async_status = 0;
+    return cg_internal_set_error(CG_OK, "");
+  }
+  if (abort_on_error) {
+    ncclCommAbort(comm->comm);
+    comm->comm = nullptr;
+  }
+  return comm_fail("communicator async error", async);
+}
+
 int cg_comm_destroy(cg_comm* comm) {
   if (!comm) return cg_internal_set_error(CG_OK, "");
   ncclResult_t r = comm->comm ? ncclCommDestroy(comm->comm) : ncclSuccess;

@@ -147,6 +147,22 @@ class RcclComm:
         _lib.check("cg_allreduce_sum_f32", self._fn(self._h, t.data_ptr(), t.numel(), s))
         return t
 
+    def nranks(self) -> int:
+        """Ranks the RCCL communicator spans (cg_comm_count = ncclCommCount)."""
+        n = ctypes.c_int(0)
+        _lib.call("cg_comm_count", self._h, ctypes.byref(n))
+        return n.value
+
+    def async_error(self, abort: bool = False) -> int:
+        """Poll the communicator's asynchronous error (cg_comm_async_error):
+        0 when healthy, else the RCCL result code (with ``abort`` the
+        communicator is aborted so blocked ranks return)."""
+        st = ctypes.c_int(0)
+        rc = _lib.lib().cg_comm_async_error(self._h, ctypes.byref(st), int(abort))
+        if rc not in (_lib.CG_OK, _lib.CG_ERR_COMM):
+            _lib.check("cg_comm_async_error", rc)
+        return st.value
+
     def close(self):
         if self._h is not None and self._h.value:
             _lib.lib().cg_comm_destroy(self._h)

@@ -297,6 +297,17 @@ class ChebRunner:
         return (self.dx if need_dx else None), self.dW
 
 
+def _saved_basis_layout(plan: ChebPlan, basis: torch.Tensor, layout: str, N: int, Fin: int, K: int,
+                        Fout: int):
+    """The basis an autograd backward hands to the C ABI: the saved one, or --
+    when the plan's path / variant was changed between forward and backward so
+    that the planes layout no longer applies -- the same values re-laid as
+    the rows layout of lib/graph_conv.py:172 (column fin*K + k)."""
+    if layout != "planes" or plan.basis_elems(N, Fin, K, Fout, "planes"):
+        return basis, layout
+    return basis.permute(1, 2, 0).reshape(N * plan.M, Fin * K).contiguous(), "rows"
+
+
 class ChebConv(torch.autograd.Function):
     """y = chebyshev5(x; L~, W, K) with the HIP forward/backward kernels."""
 
@@ -312,8 +323,11 @@ class ChebConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         basis, W = ctx.saved_tensors
+        N, Fout = dy.shape[0], W.shape[1]
+        basis, lay = _saved_basis_layout(ctx.plan, basis, ctx.layout, N, W.shape[0] // ctx.K, ctx.K,
+                                         Fout)
         dx, dW = cheb_backward(ctx.plan, dy, basis, W, ctx.K, need_dx=ctx.needs_input_grad[0],
-                               layout=ctx.layout)
+                               layout=lay)
         return dx, dW, None, None
 
 
@@ -334,8 +348,10 @@ class ChebConvAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         basis, W, y = ctx.saved_tensors
+        basis, lay = _saved_basis_layout(ctx.plan, basis, ctx.layout, dy.shape[0],
+                                         W.shape[0] // ctx.K, ctx.K, W.shape[1])
         dx, dW, dz = cheb_backward_ex(ctx.plan, dy, y, ctx.act, basis, W, ctx.K,
-                                      need_dx=ctx.needs_input_grad[0], layout=ctx.layout)
+                                      need_dx=ctx.needs_input_grad[0], layout=lay)
         return dx, dW, (dz if ctx.has_res else None), None, None, None
 
 
@@ -532,6 +548,11 @@ def lstm_hconv_step(plan: ChebPlan, h_prev, c_prev, gx, Wh, bias, K: int, gates=
         avail = planes.untyped_storage().nbytes() // 4 - planes.storage_offset()
         if K > 1 and (plane_stride < R * H or avail < need):
             raise ValueError("planes: storage too small for the K-1 planes at this stride")
+        if planes.data_ptr() % 16 or (K > 1 and plane_stride % 4):
+            raise ValueError("planes: needs a 16-byte aligned start and a stride that is a "
+                             "multiple of 4 floats (the kernel stores float4)")
+    if h_prev.data_ptr() % 16:
+        h_prev = h_prev.clone()  # float4 loads: a view at an odd offset is copied
     _lib.call("cg_lstm_hconv_step", plan.handle, N, H, int(K), LSTM_GATES[gates], _p(h_prev),
               _p(c_prev), _p(gx), _p(Wh), _p(bias), _p(c_out), _p(h_out), _p(act), _p(planes),
               int(plane_stride), _stream(h_prev))

@@ -64,18 +64,34 @@ class ChebPlan:
         self.variant = variant
         self._shape_cache = {}
 
+    # workspaces above this size are not kept by the plan (a config-D backward
+    # at N = 256 needs 51.5 GB: holding it for the plan's lifetime would pin it
+    # for every later model that shares the plan through plan_for)
+    WS_CACHE_MAX_BYTES = 1 << 30
+
     def workspace(self, nbytes: int, device, stream_id: int):
-        """A device workspace of at least ``nbytes`` owned by the plan and reused
-        by every call enqueued on the same stream (stream order makes the reuse
-        safe: a call's workspace is dead once the call has executed).  Grown,
-        never shrunk; one buffer per (device, stream)."""
+        """A device workspace of at least ``nbytes``.  Up to WS_CACHE_MAX_BYTES
+        it is owned by the plan and reused by every call enqueued on the same
+        stream (stream order makes the reuse safe: a call's workspace is dead
+        once the call has executed); grown, never shrunk, one buffer per
+        (device, stream) -- ``release_workspace()`` frees them.  Larger requests
+        get a buffer of their own that the caching allocator takes back once the
+        call's stream has used it (torch's stream-ordered frees)."""
         import torch
+        nbytes = max(int(nbytes), 256)
+        if nbytes > self.WS_CACHE_MAX_BYTES:
+            return torch.empty(nbytes, device=device, dtype=torch.uint8)
         key = (str(device), int(stream_id))
         buf = self._ws.get(key)
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(int(nbytes), 256), device=device, dtype=torch.uint8)
+            buf = torch.empty(nbytes, device=device, dtype=torch.uint8)
             self._ws[key] = buf
         return buf
+
+    def release_workspace(self):
+        """Drop the plan's cached workspaces (e.g. after a large streaming call,
+        or when the stream they were keyed on is gone)."""
+        self._ws = {}
 
     def _shape_info(self, N, Fin, K, Fout):
         key = (int(N), int(Fin), int(K), int(Fout))

@@ -116,6 +116,7 @@ int cg_cheb_forward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fo
  *   dx [N][M][Fin]  (NULL to skip), dW [Fin*K][Fout]  (overwritten, not accumulated;
  *   NULL to skip -- e.g. a recurrent caller that sums dW over time steps with
  *   one cg_weight_grad call; dx and dW may not both be NULL)
+ *   basis may be NULL when dW is NULL (a dx-only call never reads it).
  * dW = basis^T dy ; dBasis = dy W^T ; reverse recurrence over L~^T.
  * ------------------------------------------------------------------------- */
 int cg_cheb_backward(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
@@ -407,6 +408,16 @@ int cg_comm_unique_id(unsigned char id[128]);
 int cg_comm_init(cg_comm** comm, int nranks, int rank, const unsigned char id[128], int device);
 int cg_allreduce_sum_f32(cg_comm* comm, float* buf, size_t count, void* stream);
 int cg_comm_destroy(cg_comm* comm);
+/* Ranks the communicator spans (ncclCommCount): lets a caller prove the
+ * exchange it times really ran over N ranks. */
+int cg_comm_count(const cg_comm* comm, int* nranks);
+/* Asynchronous communicator error (ncclCommGetAsyncError), polled by the
+ * caller after a failed or timed-out step (SURVEY.md §5 failure detection):
+ * *async_status = 0 when healthy, else the RCCL result code; the status
+ * returned is CG_ERR_COMM (message in cg_last_error()) when an error is
+ * pending.  With abort_on_error != 0 a pending error also aborts the
+ * communicator (ncclCommAbort) so blocked ranks return. */
+int cg_comm_async_error(cg_comm* comm, int* async_status, int abort_on_error);
 
 #ifdef __cplusplus
 }

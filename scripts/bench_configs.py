@@ -31,7 +31,11 @@ from cnn_graph_amd import ops  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
 
-def ev_ms(fn, reps=5, rounds=3):
+ROUNDS = 3
+
+
+def ev_ms(fn, reps=5, rounds=None):
+    rounds = ROUNDS if rounds is None else rounds
     vals = []
     for _ in range(rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -138,7 +142,10 @@ def main():
     ap.add_argument("--variant", default="auto", help="plan variant (auto / narrow / ...)")
     ap.add_argument("--layout", default="rows", choices=["rows", "planes"],
                     help="basis layout of the C1/C2/D filters (planes: where it applies)")
+    ap.add_argument("--rounds", type=int, default=3, help="timed rounds per measurement (median)")
     args = ap.parse_args()
+    global ROUNDS
+    ROUNDS = args.rounds
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     from cnn_graph_amd.graph import rescale_L

@@ -236,6 +236,35 @@ def test_autograd_uses_planes_with_rows_gradients(dev):
     assert O.normwise_err(y.detach().cpu().numpy().reshape(N * M, Fout), y64) < 1e-5
 
 
+def test_autograd_planes_basis_after_path_change(dev):
+    """The plan's path is changed between an autograd forward (streaming,
+    planes-layout basis saved) and its backward (now resident, where the
+    planes layout does not apply): the backward re-lays the saved basis as
+    rows and matches the streaming rows-layout gradients."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden("golden_A.npz"))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    plan = ChebPlan(Lt, device=0, path="stream")
+    N, Fin, K, Fout = 4, 16, 3, 16
+    assert ops.basis_layout_for(plan, N, Fin, K, Fout) == "planes"
+    rng = np.random.default_rng(19)
+    x = _t(rng.standard_normal((N, M, Fin)), dev).requires_grad_(True)
+    W = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev).requires_grad_(True)
+    dy = _t(rng.standard_normal((N, M, Fout)), dev)
+    basis, _ = ops.cheb_forward(plan, x.detach(), W.detach(), K)
+    dx_r, dW_r = ops.cheb_backward(plan, dy, basis, W.detach(), K)
+    y = ops.cheb_conv(x, W, plan, K)
+    plan.set_path("auto")
+    assert plan.query_path(N, Fin, K, Fout) == "resident"
+    assert ops.basis_layout_for(plan, N, Fin, K, Fout) == "rows"
+    y.backward(dy)
+    torch.cuda.synchronize()
+    assert O.normwise_err(x.grad.cpu().numpy(), dx_r.cpu().numpy().astype(np.float64)) < 1e-5
+    assert O.normwise_err(W.grad.cpu().numpy(), dW_r.cpu().numpy().astype(np.float64)) < 1e-5
+
+
 def test_planes_layout_skewed_graph(dev):
     """Planes vs rows on a hub-and-spoke graph whose row lengths are skewed
     enough for the degree-sorted row order (max row > 2 * mean + 8): the

@@ -119,6 +119,32 @@ def test_config_c_wide_vs_narrow_layout(dev, graph_c, N, Fin, K, Fout):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("N,Fin,K,Fout", [(128, 1, 5, 32), (64, 2, 3, 16)])
+def test_dx_only_backward_without_basis(dev, graph_c, N, Fin, K, Fout):
+    """A dx-only backward (dW not wanted) may pass basis = NULL (the recurrent
+    callers do): on the wide-column shapes whose dy pass also computes dW
+    partials (Fin < 8, Fin*K <= 32, Fout % 8 == 0, <= 32) the basis loads are
+    skipped; dx is bitwise the dx of the call that had the basis."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    rp, ci, v, M = graph_c["Lt_rowptr"], graph_c["Lt_col"], graph_c["Lt_val"], graph_c["M"]
+    rng = np.random.default_rng(N + Fin)
+    x = rng.random((N, M, Fin), dtype=np.float32)
+    W = (rng.standard_normal((Fin * K, Fout)) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((N, M, Fout)).astype(np.float32)
+    plan = ChebPlan(scipy.sparse.csr_matrix((v, ci, rp), shape=(M, M)), device=0)
+    assert plan.query_path(N, Fin, K, Fout) == "stream"
+    basis, _ = ops.cheb_forward(plan, t(x, dev), t(W, dev), K)
+    dx_ref, _ = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), K)
+    dx, dW = ops.cheb_backward(plan, t(dy, dev), None, t(W, dev), K, need_dW=False)
+    torch.cuda.synchronize()
+    assert dW is None
+    assert torch.equal(dx, dx_ref)
+    ob, _ = O.cheb_forward(x, rp, ci, v, W, K)
+    odx, _ = O.cheb_backward(dy, ob, W, rp, ci, v, N, M, Fin, K)
+    assert O.normwise_err(dx.cpu().numpy(), odx) < TOL
+
+
 @pytest.mark.parametrize("N,Fin,K,Fout", [(128, 1, 5, 32), (8, 32, 5, 32)])
 def test_config_c_batch_vs_oracle(dev, graph_c, N, Fin, K, Fout):
     """Config C layer 1 at its full batch (N=128) and a layer-2 shape (Fin=32)."""
