@@ -323,6 +323,25 @@ hipError_t launch_lstm_hstep(int gates, int N, int M, int K, const int* rowptr, 
                              const float* gx, const float* Wh, const float* bias, float* c_out,
                              float* h_out, float* act, float* planes, int64_t plane,
                              hipStream_t s);
+// The gconv-LSTM layer forward over all T steps in ONE cooperative launch and
+// the BPTT step in one launch (lstm_seq.hip).  H == 32, M <= 1024.
+size_t lstm_seq_lds(int M, int K, int64_t nnz);
+bool lstm_seq_ok(int M, int H, int K, int64_t nnz);
+size_t lstm_bstep_lds(int M, int K);
+bool lstm_bstep_ok(int M, int H, int K);
+// workgroup pairs of the persistent forward (min(N, CUs / 2))
+int lstm_seq_pairs(int N, int device);
+// flags: 2P + 1 ints (pair step counters, then the status word), zeroed here
+hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, const int* rowptr,
+                           const int* col, const float* val, const float* gx, const float* Wh,
+                           const float* bias, const float* h0, const float* c0, float* hs,
+                           float* cs, float* act, float* planes, int64_t pstride, int* flags,
+                           int* status, int P, hipStream_t s);
+hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr, const int* tcol,
+                             const float* tval, const float* dh, const float* dh_rec,
+                             const float* dc, const float* act, const float* c_prev,
+                             const float* c_out, const float* Wh, float* dpre, float* dc_prev,
+                             float* dh_prev, hipStream_t s);
 // Column sums of A [R][C] as [colsum_chunks(R)][C] partial slabs.
 int colsum_chunks(int64_t R);
 hipError_t launch_colsum_slabs(const float* A, int64_t R, int C, float* slab, hipStream_t s);

@@ -1406,6 +1406,99 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
   return ok();
 }
 
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int cg_lstm_seq_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* supported) {
+  if (!plan || !supported) return fail(CG_ERR_ARG, "lstm_seq_supported: null argument");
+  *supported = (cg::lstm_seq_ok(plan->M, H, K, plan->nnz) && cg::lstm_bstep_ok(plan->M, H, K)) ? 1 : 0;
+  return ok();
+}
+
+int cg_lstm_seq_workspace_bytes(const cg_plan* plan, int32_t N, size_t* bytes) {
+  if (!plan || !bytes || N < 1) return fail(CG_ERR_ARG, "lstm_seq_workspace_bytes: bad arguments");
+  *bytes = al256(sizeof(int) * (size_t(2) * cg::lstm_seq_pairs(N, plan->device) + 1));
+  return ok();
+}
+
+int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t K, int32_t gates,
+                        const float* gx, const float* Wh, const float* bias, const float* h0,
+                        const float* c0, float* hs, float* cs, float* act, float* planes,
+                        int64_t plane_stride, void* workspace, size_t ws_bytes, void* stream) {
+  int rc = check_lstm(int64_t(T) * N * (plan ? plan->M : 1), H, gates);
+  if (rc) return rc;
+  if (!plan || T < 1 || N < 1 || K < 1) return fail(CG_ERR_ARG, "lstm_seq_forward: bad plan / T / N / K");
+  if (!gx || !Wh || !hs || !cs) return fail(CG_ERR_ARG, "lstm_seq_forward: null gx / Wh / hs / cs");
+  if (!cg::lstm_seq_ok(plan->M, H, K, plan->nnz))
+    return fail(CG_ERR_UNSUPPORTED, "lstm_seq_forward: needs H = 32, M <= 1024 and L~ plus the "
+                                    "weights in LDS (M=%d nnz=%lld H=%d K=%d)",
+                plan->M, (long long)plan->nnz, H, K);
+  const int64_t R = int64_t(T) * N * plan->M;
+  if (planes && K > 1 && plane_stride < R * H)
+    return fail(CG_ERR_ARG, "lstm_seq_forward: plane stride %lld < T*N*M*H", (long long)plane_stride);
+  if (!al16(gx) || !al16(hs) || !al16(cs) || (act && !al16(act)) || (planes && !al16(planes)) ||
+      (h0 && !al16(h0)) || (c0 && !al16(c0)) || (bias && !al16(bias)) ||
+      (planes && K > 1 && (plane_stride & 3)))
+    return fail(CG_ERR_ARG, "lstm_seq_forward: tensors must be 16-byte aligned (float4 access), "
+                            "plane stride a multiple of 4");
+  const void* outs[] = {hs, cs, act, planes};
+  const void* ins[] = {gx, Wh, bias, h0, c0};
+  for (const void* o : outs)
+    for (const void* i : ins)
+      if (o && o == i) return fail(CG_ERR_ARG, "lstm_seq_forward: outputs must not alias inputs");
+  size_t need = 0;
+  if ((rc = cg_lstm_seq_workspace_bytes(plan, N, &need))) return rc;
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "lstm_seq_forward: workspace %zu < %zu bytes", ws_bytes, need);
+  if ((rc = check_device(plan))) return rc;
+  const int P = cg::lstm_seq_pairs(N, plan->device);
+  int* flags = static_cast<int*>(workspace);
+  CG_HIP(cg::launch_lstm_seq(gates, T, N, plan->M, K, plan->nnz, plan->rowptr, plan->col, plan->val,
+                             gx, Wh, bias, h0, c0, hs, cs, act, planes, plane_stride, flags,
+                             flags + 2 * P, P, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,
+                       void* stream) {
+  if (!plan || !workspace || !status || N < 1) return fail(CG_ERR_ARG, "lstm_seq_status: bad arguments");
+  const int P = cg::lstm_seq_pairs(N, plan->device);
+  int v = 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  CG_HIP(hipMemcpyAsync(&v, static_cast<const int*>(workspace) + 2 * P, sizeof(int),
+                        hipMemcpyDeviceToHost, s));
+  CG_HIP(hipStreamSynchronize(s));
+  *status = v;
+  if (v) return fail(CG_ERR_HIP, "lstm_seq_forward: a workgroup pair hand-off timed out");
+  return ok();
+}
+
+int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,
+                     const float* dh_rec, const float* dc, const float* act, const float* c_prev,
+                     const float* c_out, const float* Wh, float* dpre, float* dc_prev,
+                     float* dh_prev, void* stream) {
+  int rc = check_lstm(int64_t(N) * (plan ? plan->M : 1), H, gates);
+  if (rc) return rc;
+  if (!plan || N < 1 || K < 1) return fail(CG_ERR_ARG, "lstm_bwd_step: bad plan / N / K");
+  if (!act || !c_out || !Wh || !dpre || !dh_prev)
+    return fail(CG_ERR_ARG, "lstm_bwd_step: null act / c_out / Wh / dpre / dh_prev");
+  if (!cg::lstm_bstep_ok(plan->M, H, K))
+    return fail(CG_ERR_UNSUPPORTED, "lstm_bwd_step: needs H = 32, M <= 1024, K <= 4 (M=%d H=%d K=%d)",
+                plan->M, H, K);
+  const void* all[] = {dh, dh_rec, dc, act, c_prev, c_out, dpre, dc_prev, dh_prev};
+  for (const void* p : all)
+    if (p && !al16(p)) return fail(CG_ERR_ARG, "lstm_bwd_step: tensors must be 16-byte aligned");
+  const void* outs[] = {dpre, dc_prev, dh_prev};
+  const void* ins[] = {dh, dh_rec, dc, act, c_prev, c_out, Wh};
+  for (const void* o : outs)
+    for (const void* i : ins)
+      if (o && o == i) return fail(CG_ERR_ARG, "lstm_bwd_step: outputs must not alias inputs");
+  if ((rc = check_device(plan))) return rc;
+  CG_HIP(cg::launch_lstm_bstep(gates, N, plan->M, K, plan->trowptr, plan->tcol, plan->tval, dh, dh_rec,
+                               dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev,
+                               reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
 int cg_perm_gather(const float* x, const int32_t* perm, int32_t N, int32_t M_in, int32_t M_out,
                    int32_t F, float* out, void* stream) {
   if (!x || !perm || !out || N < 1 || M_in < 1 || M_out < 1 || F < 1)

@@ -1,0 +1,628 @@
+// gconv-LSTM layer on gfx950: the T-step forward in ONE persistent launch and
+// the backprop-through-time step in ONE launch per step
+// (lib/gconv_lstm.py:609-627 glstm_layer -> static_rnn over GConvLSTMCell,
+// :77-221), H = 32 hidden units, M <= 1024 vertices.
+//
+// Per time step the cell computes (x-conv gx precomputed for all steps at
+// once by the time-batched chebyshev5 call):
+//   T_0 = h, T_1 = L~ h, T_k = 2 L~ T_{k-1} - T_{k-2}       (cheby_conv, :183-207)
+//   a = (gx + sum_k T_k Wh_k) + b
+//   z = tan(a_z), i = sigmoid(a_i), f = sigmoid(a_f), o = tanh(a_o)   (reference)
+//   c' = f c + i z ;  h' = o tanh(c')                              (:215, :218)
+//
+// k_lstm_seq (forward, all T steps, one cooperative launch)
+//   Two 512-thread workgroups per sample (8 waves, 256 registers per lane): workgroup u owns hidden units
+//   [16u, 16u + 16) (64 of the 128 gate columns); blocks b and b + 8 share an
+//   XCD under round-robin placement, so a pair's hand-off stays in one L2
+//   (speed only -- the hand-off protocol is agent-scope and placement-free).
+//   Each workgroup runs the whole Chebyshev recurrence of h (one 8-channel
+//   quarter at a time, two [M][8] LDS slots, CSR of L~ staged once in LDS)
+//   and the gate contraction on v_mfma_f32_32x32x2_f32 TRANSPOSED
+//   (gates x rows = Wh^T T^T): the B operand is the lane's own T_k values
+//   straight from the SpMM (no LDS read), and the accumulator leaves each
+//   lane ALL FOUR gates of 4 units of one row, so the LSTM update is in-lane
+//   (no shuffles); c_{t-1} is read back by the lane that stored it.
+//   Hand-off per step: every lane stores its h' (the output hs[t]) with sc1
+//   (write-through) stores, each wave drains (s_waitcnt vmcnt(0)), the
+//   workgroup barrier, then ONE lane stores the step counter sc1 into the
+//   pair's flag; the partner polls it (sc1 loads, s_sleep, bounded by a
+//   wall-clock timeout that sets a status word and ends the launch), joins a
+//   barrier, and reads the other half of h with sc1 loads
+//   (MI355X_MICROARCH.md §inter-workgroup visibility, table row 1).  A
+//   workgroup does its OWN two quarters first, so the partner's half has
+//   half a step to arrive.  All workgroups are co-resident (at most one
+//   pair per two CUs); more samples than pairs are
+//   processed by the same pairs in turn.  The grid never exceeds the
+//   occupancy query's resident workgroups (checked at launch).
+//
+// k_lstm_bstep (backward, one launch per step, two workgroups per sample)
+//   dpre = TF autodiff of the pointwise update (the expressions of
+//   lstm.hip::k_lstm_bwd, so dpre is bitwise the unfused kernel's), then
+//   D_k = dpre Wh_k^T on v_mfma_f32_16x16x4_f32 (again transposed: each lane
+//   computes dpre for 8 units x 4 gates of one row and feeds it as the B
+//   operand), then the reverse (Clenshaw) recurrence over the explicit L~^T
+//   G_{K-1} = D_{K-1}, G_k = (D_k + c L~^T G_{k+1}) - G_{k+2} (c = 2, 1 at
+//   k = 0) in two [M][16] LDS slots; workgroup u owns h channels
+//   [16u, 16u + 16) of dh_prev = G_0 and stores the dpre / dc_prev of its
+//   units.  The h-weight gradient is summed afterwards per Chebyshev order
+//   over all steps from the forward's planes (one GEMM per order).
+#include "cg_internal.h"
+
+namespace cg {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kST = 512;   // threads per workgroup: 8 waves, 2 per SIMD (256 VGPRs)
+constexpr int kH = 32;     // hidden units
+constexpr int kQ = 8;      // channels per forward SpMM pass (a quarter of H)
+constexpr int kBS = 16;    // channels per backward workgroup (half of H)
+constexpr int kRT = 4;     // forward: 32-row tiles per wave (8 waves x 4 x 32 = 1024 rows)
+constexpr int kRB = 8;     // backward: 16-row tiles per wave (8 x 8 x 16 = 1024 rows)
+constexpr int kSeqStaticLds = 64;  // k_lstm_seq's static __shared__ bytes (upper bound)
+
+__device__ __forceinline__ float sigm(float a) { return 1.f / (1.f + expf(-a)); }
+
+// agent-scope relaxed accesses: global_load/store ... sc1 (L1 bypass)
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(const_cast<float*>(p)),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct SeqArgs {
+  const int* rowptr;  // L~ (CSR, sorted columns)
+  const int* col;
+  const float* val;
+  int M, Mr, K, N, T, gates, nnz, P, pair_xcd;
+  const float* gx;    // [T][N][M][128] x-conv gate pre-activations
+  const float* Wh;    // [K*32][128], row c*K + k
+  const float* bias;  // [128] or NULL
+  const float* h0;    // [N][M][32] or NULL (zero state: step 0 has no h-conv)
+  const float* c0;    // [N][M][32] or NULL
+  float* hs;          // [T][N][M][32]
+  float* cs;          // [T][N][M][32]
+  float* act;         // [T][N][M][128] gate activations, or NULL
+  float* planes;      // T_k of h_{t-1} at (k-1)*pstride + [T][N][M][32], or NULL
+  int64_t pstride;
+  int* flags;         // [P][2] step counters (zeroed before the launch)
+  int* status;        // [1] 0 = ok, 1 = a hand-off timed out
+  unsigned long long timeout;  // wall-clock ticks
+};
+
+__global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int s_abort;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const int M = A.M, K = A.K, N = A.N, T = A.T;
+  int pair, u;
+  if (A.pair_xcd) {
+    const int b = blockIdx.x;
+    pair = (b >> 4) * 8 + (b & 7);
+    u = (b >> 3) & 1;
+  } else {
+    pair = blockIdx.x >> 1;
+    u = blockIdx.x & 1;
+  }
+  float* slot0 = smem;
+  float* slot1 = smem + A.Mr * kQ;
+  float* s_W = slot1 + A.Mr * kQ;  // [K][q 4][s 4][hh 2][ct 2][i 32]
+  float* s_b = s_W + K * 2048;  // [128] bias (zeros when NULL)
+  float* s_val = s_b + 128;
+  unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
+  // A operands of the transposed contraction: lane (i, hh) of MFMA step s in
+  // quarter q, order k holds Wh[(8q + 4hh + s) K + k][gate column of tile
+  // row i] -- tile ct's rows i = 8 g + m are gate g, unit 16u + 8ct + m
+  for (int e = tid; e < K * 2048; e += kST) {
+    const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3;
+    const int q = (e >> 9) & 3, k = e >> 11;
+    const int ch = 8 * q + 4 * h2 + s;
+    const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
+    s_W[e] = A.Wh[int64_t(ch * K + k) * 128 + gcol];
+  }
+  for (int e = tid; e < 128; e += kST) s_b[e] = A.bias ? A.bias[e] : 0.f;
+  for (int e = tid; e < A.nnz; e += kST) {
+    s_val[e] = A.val[e];
+    s_col[e] = static_cast<unsigned short>(A.col[e]);
+  }
+  if (tid == 0) s_abort = 0;
+  int row[kRT], rb[kRT], re[kRT];
+  bool rv[kRT];
+#pragma unroll
+  for (int rt = 0; rt < kRT; ++rt) {
+    row[rt] = (wave + 8 * rt) * 32 + j;
+    rv[rt] = row[rt] < M;
+    rb[rt] = rv[rt] ? A.rowptr[row[rt]] : 0;
+    re[rt] = rv[rt] ? A.rowptr[row[rt] + 1] : 0;
+  }
+  __syncthreads();
+
+  int* my_flag = A.flags + 2 * pair + u;
+  const int* partner_flag = A.flags + 2 * pair + (1 - u);
+  for (int n = pair, it = 0; n < N; n += A.P, ++it) {
+    const int base = it * T;
+    for (int t = 0; t < T; ++t) {
+      f32x16 acc[kRT][2];
+#pragma unroll
+      for (int rt = 0; rt < kRT; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[rt][ct][e] = 0.f;
+      if (t > 0 || A.h0) {
+        const float* hsrc = (t == 0) ? A.h0 + int64_t(n) * M * kH
+                                     : A.hs + (int64_t(t - 1) * N + n) * M * kH;
+        for (int qi = 0; qi < 4; ++qi) {
+          const int q = (2 * u + qi) & 3;  // own quarters first
+          if (qi == 2 && t > 0) {
+            // the partner's half of h_{t-1}: wait for its step t-1 counter
+            if (tid == 0) {
+              const int need = base + t;
+              const unsigned long long t0 = wall_clock64();
+              while (__hip_atomic_load(const_cast<int*>(partner_flag), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT) < need) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > A.timeout) {
+                  s_abort = 1;
+                  __hip_atomic_store(A.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  break;
+                }
+              }
+            }
+            __syncthreads();
+            if (s_abort) return;  // every thread of the workgroup returns here
+          }
+          // T_0 quarter: registers + slot 0
+          float Tc[kRT][4];
+#pragma unroll
+          for (int rt = 0; rt < kRT; ++rt) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) Tc[rt][s] = 0.f;
+            if (rv[rt]) {
+              const float* p = hsrc + int64_t(row[rt]) * kH + 8 * q + 4 * hh;
+              if (t > 0) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) Tc[rt][s] = ld_sc1(p + s);
+              } else {
+                const float4 v = *reinterpret_cast<const float4*>(p);
+                Tc[rt][0] = v.x;
+                Tc[rt][1] = v.y;
+                Tc[rt][2] = v.z;
+                Tc[rt][3] = v.w;
+              }
+              *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) =
+                  make_float4(Tc[rt][0], Tc[rt][1], Tc[rt][2], Tc[rt][3]);
+            }
+          }
+          __syncthreads();
+          for (int k = 0; k < K; ++k) {
+            // gates^T += Wh_k^T T_k^T over this quarter's 8 channels
+            const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
+#pragma unroll
+              for (int rt = 0; rt < kRT; ++rt) {
+                acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, Tc[rt][s], acc[rt][0], 0, 0, 0);
+                acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, Tc[rt][s], acc[rt][1], 0, 0, 0);
+              }
+            }
+            if (k + 1 < K) {
+              // T_{k+1} of this lane's rows / channels: CSR order from +0
+              const float* cur = (k & 1) ? slot1 : slot0;
+              float* nxt = (k & 1) ? slot0 : slot1;
+#pragma unroll
+              for (int rt = 0; rt < kRT; ++rt) {
+                if (!rv[rt]) continue;
+                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+                for (int jj = rb[rt]; jj < re[rt]; ++jj) {
+                  const float w = s_val[jj];
+                  const float4 g = *reinterpret_cast<const float4*>(cur + int(s_col[jj]) * kQ + 4 * hh);
+                  s0 = s0 + w * g.x;
+                  s1 = s1 + w * g.y;
+                  s2 = s2 + w * g.z;
+                  s3 = s3 + w * g.w;
+                }
+                float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kQ + 4 * hh);
+                if (k >= 1) {  // T_{k-1} of this row: the slot being overwritten
+                  const float4 p = *own;
+                  s0 = 2.f * s0 - p.x;
+                  s1 = 2.f * s1 - p.y;
+                  s2 = 2.f * s2 - p.z;
+                  s3 = 2.f * s3 - p.w;
+                }
+                const float4 o = make_float4(s0, s1, s2, s3);
+                *own = o;
+                if (A.planes && (q >> 1) == u)
+                  *reinterpret_cast<float4*>(A.planes + int64_t(k) * A.pstride +
+                                             ((int64_t(t) * N + n) * M + row[rt]) * kH + 8 * q +
+                                             4 * hh) = o;
+                Tc[rt][0] = s0;
+                Tc[rt][1] = s1;
+                Tc[rt][2] = s2;
+                Tc[rt][3] = s3;
+              }
+              __syncthreads();
+            }
+          }
+        }
+      }
+      // gate update: lane (row, hh) of tile (rt, ct) holds gates g = 0..3 of
+      // units 16u + 8ct + 4hh + m in acc[rt][ct][4g + m]
+#pragma unroll
+      for (int rt = 0; rt < kRT; ++rt) {
+        if (!rv[rt]) continue;
+        const int64_t rr = (int64_t(t) * N + n) * M + row[rt];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const int u0 = 16 * u + 8 * ct + 4 * hh;
+          float4 gv[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            gv[g] = *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
+          // c_{t-1}: this lane's own store of the previous step (same address,
+          // same lane), or the initial state
+          float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (t > 0)
+            cv = *reinterpret_cast<const float4*>(A.cs + (rr - int64_t(N) * M) * kH + u0);
+          else if (A.c0)
+            cv = *reinterpret_cast<const float4*>(A.c0 + (int64_t(n) * M + row[rt]) * kH + u0);
+          float c[4] = {cv.x, cv.y, cv.z, cv.w};
+          float hn[4], zz[4], ii[4], ff[4], oo[4];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const float gz = (&gv[0].x)[m], gi = (&gv[1].x)[m], gf = (&gv[2].x)[m],
+                        go = (&gv[3].x)[m];
+            float az = gz + acc[rt][ct][m], ai = gi + acc[rt][ct][4 + m];
+            float af = gf + acc[rt][ct][8 + m], ao = go + acc[rt][ct][12 + m];
+            if (A.bias) {
+              az = az + s_b[u0 + m];
+              ai = ai + s_b[32 + u0 + m];
+              af = af + s_b[64 + u0 + m];
+              ao = ao + s_b[96 + u0 + m];
+            }
+            const float z = A.gates == 0 ? tanf(az) : tanhf(az);
+            const float ig = sigm(ai), fg = sigm(af);
+            const float o = A.gates == 0 ? tanhf(ao) : sigm(ao);
+            const float cn = fg * c[m] + ig * z;
+            c[m] = cn;
+            hn[m] = o * tanhf(cn);
+            zz[m] = z;
+            ii[m] = ig;
+            ff[m] = fg;
+            oo[m] = o;
+          }
+          *reinterpret_cast<float4*>(A.cs + rr * kH + u0) =
+              make_float4(c[0], c[1], c[2], c[3]);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) st_sc1(A.hs + rr * kH + u0 + m, hn[m]);
+          if (A.act) {
+            float* ap = A.act + rr * 128 + u0;
+            *reinterpret_cast<float4*>(ap) = make_float4(zz[0], zz[1], zz[2], zz[3]);
+            *reinterpret_cast<float4*>(ap + 32) = make_float4(ii[0], ii[1], ii[2], ii[3]);
+            *reinterpret_cast<float4*>(ap + 64) = make_float4(ff[0], ff[1], ff[2], ff[3]);
+            *reinterpret_cast<float4*>(ap + 96) = make_float4(oo[0], oo[1], oo[2], oo[3]);
+          }
+        }
+      }
+      // publish h_t: every wave drains its stores, then one flag store
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(my_flag, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+struct BStepArgs {
+  const int* trowptr;  // L~^T (exact transpose, CSR)
+  const int* tcol;
+  const float* tval;
+  int M, Mr, N, gates, pair_xcd;
+  const float* dh;      // [N][M][32] gradient of h' from above, or NULL
+  const float* dh_rec;  // [N][M][32] gradient of h' from step t+1's h-conv, or NULL
+  const float* dc;      // [N][M][32] gradient of c', or NULL
+  const float* act;     // [N][M][128]
+  const float* c_prev;  // [N][M][32] or NULL (zero state)
+  const float* c_out;   // [N][M][32]
+  const float* Wh;      // [K*32][128]
+  float* dpre;          // [N][M][128]
+  float* dc_prev;       // [N][M][32] or NULL
+  float* dh_prev;       // [N][M][32]
+};
+
+template <int K>
+__global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int jr = lane & 15, q = lane >> 4;
+  const int M = A.M;
+  int n, u;
+  if (A.pair_xcd) {
+    const int b = blockIdx.x;
+    n = (b >> 4) * 8 + (b & 7);
+    u = (b >> 3) & 1;
+  } else {
+    n = blockIdx.x >> 1;
+    u = blockIdx.x & 1;
+  }
+  float* slotA = smem;
+  float* slotB = smem + A.Mr * kBS;
+  float* s_W = slotB + A.Mr * kBS;  // [K][s 32][q 4][i 16]
+  // A operand of MFMA step s, order o: lane (i, q) holds Wh[(16u + i) K + o][g]
+  // with g the gate column (s % 4) * 32 + 8q + s / 4 -- the column whose dpre
+  // lane (row, q) supplies as the B operand at that step
+  for (int e = tid; e < K * 2048; e += kST) {
+    const int i = e & 15, qq = (e >> 4) & 3, s = (e >> 6) & 31, o = e >> 11;
+    s_W[e] = A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
+  }
+  __syncthreads();
+  f32x4 acc[kRB][K];
+#pragma unroll
+  for (int rt = 0; rt < kRB; ++rt)
+#pragma unroll
+    for (int o = 0; o < K; ++o) acc[rt][o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool ref = A.gates == 0;
+  const bool own = (q >> 1) == u;  // this lane's units are stored by this workgroup
+  // phase A: dpre of units 8q .. 8q+7 of rows wave*128 + 16 rt + jr, and D_o
+#pragma unroll
+  for (int rt = 0; rt < kRB; ++rt) {
+    const int row = wave * 128 + rt * 16 + jr;
+    float dp[4][8];
+    if (row < M) {
+      const int64_t rr = int64_t(n) * M + row;
+      const float* ap = A.act + rr * 128 + 8 * q;
+      const int64_t hb = rr * kH + 8 * q;
+      float av[4][8], cp[8], co[8], dhv[8], dcv[8];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 x0 = *reinterpret_cast<const float4*>(ap + g * 32);
+        const float4 x1 = *reinterpret_cast<const float4*>(ap + g * 32 + 4);
+        av[g][0] = x0.x; av[g][1] = x0.y; av[g][2] = x0.z; av[g][3] = x0.w;
+        av[g][4] = x1.x; av[g][5] = x1.y; av[g][6] = x1.z; av[g][7] = x1.w;
+      }
+      auto ld8 = [&](const float* base, float* out) {
+        if (base) {
+          const float4 x0 = *reinterpret_cast<const float4*>(base + hb);
+          const float4 x1 = *reinterpret_cast<const float4*>(base + hb + 4);
+          out[0] = x0.x; out[1] = x0.y; out[2] = x0.z; out[3] = x0.w;
+          out[4] = x1.x; out[5] = x1.y; out[6] = x1.z; out[7] = x1.w;
+        } else {
+#pragma unroll
+          for (int m = 0; m < 8; ++m) out[m] = 0.f;
+        }
+      };
+      ld8(A.c_prev, cp);
+      ld8(A.c_out, co);
+      ld8(A.dh, dhv);
+      ld8(A.dc, dcv);
+      float dhr[8];
+      ld8(A.dh_rec, dhr);
+      float dcp[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        // the expressions (and their order) of lstm.hip::k_lstm_bwd
+        const float z = av[0][m], i = av[1][m], f = av[2][m], o = av[3][m];
+        const float tc = tanhf(co[m]);
+        float dh = A.dh ? dhv[m] : 0.f;
+        if (A.dh_rec) dh = dh + dhr[m];
+        float dcn = dh * o * (1.f - tc * tc);
+        if (A.dc) dcn = dcn + dcv[m];
+        const float d_o = dh * tc;
+        const float d_i = dcn * z, d_z = dcn * i, d_f = dcn * cp[m];
+        dp[0][m] = ref ? d_z * (1.f + z * z) : d_z * (1.f - z * z);
+        dp[1][m] = d_i * (i * (1.f - i));
+        dp[2][m] = d_f * (f * (1.f - f));
+        dp[3][m] = ref ? d_o * (1.f - o * o) : d_o * (o * (1.f - o));
+        dcp[m] = dcn * f;
+      }
+      if (own) {
+        float* dq = A.dpre + rr * 128 + 8 * q;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          *reinterpret_cast<float4*>(dq + g * 32) = make_float4(dp[g][0], dp[g][1], dp[g][2], dp[g][3]);
+          *reinterpret_cast<float4*>(dq + g * 32 + 4) =
+              make_float4(dp[g][4], dp[g][5], dp[g][6], dp[g][7]);
+        }
+        if (A.dc_prev) {
+          *reinterpret_cast<float4*>(A.dc_prev + hb) = make_float4(dcp[0], dcp[1], dcp[2], dcp[3]);
+          *reinterpret_cast<float4*>(A.dc_prev + hb + 4) = make_float4(dcp[4], dcp[5], dcp[6], dcp[7]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int m = 0; m < 8; ++m) dp[g][m] = 0.f;
+    }
+    // D_o^T[channel 16u + i][row] += Wh_o[.][g] dpre[row][g]
+#pragma unroll
+    for (int o = 0; o < K; ++o) {
+      const float* wo = s_W + o * 2048 + lane;
+#pragma unroll
+      for (int s = 0; s < 32; ++s)
+        acc[rt][o] = __builtin_amdgcn_mfma_f32_16x16x4f32(wo[s * 64], dp[s & 3][s >> 2], acc[rt][o],
+                                                          0, 0, 0);
+    }
+  }
+  // phase B: lane (row, q) holds D_o[row][16u + 4q + r] in acc[rt][o][r]
+  float G1[kRB][4], G2[kRB][4];
+#pragma unroll
+  for (int rt = 0; rt < kRB; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      G1[rt][r] = acc[rt][K - 1][r];
+      G2[rt][r] = 0.f;
+    }
+  if (K > 1) {
+#pragma unroll
+    for (int rt = 0; rt < kRB; ++rt) {
+      const int row = wave * 128 + rt * 16 + jr;
+      if (row < M)
+        *reinterpret_cast<float4*>(slotA + row * kBS + 4 * q) =
+            make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = K - 2; k >= 0; --k) {
+    const float* cur = ((K - 2 - k) & 1) ? slotB : slotA;
+    float* nxt = ((K - 2 - k) & 1) ? slotA : slotB;
+    const float cc = k >= 1 ? 2.f : 1.f;
+#pragma unroll
+    for (int rt = 0; rt < kRB; ++rt) {
+      const int row = wave * 128 + rt * 16 + jr;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      if (row < M) {
+        const int j0 = A.trowptr[row], j1 = A.trowptr[row + 1];
+        for (int jb = j0; jb < j1; jb += 8) {
+          int cidx[8];
+          float ww[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int jj = (jb + e < j1) ? jb + e : j1 - 1;
+            cidx[e] = A.tcol[jj];
+            ww[e] = A.tval[jj];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float4 g = *reinterpret_cast<const float4*>(cur + cidx[e] * kBS + 4 * q);
+            if (jb + e < j1) {
+              s0 = s0 + ww[e] * g.x;
+              s1 = s1 + ww[e] * g.y;
+              s2 = s2 + ww[e] * g.z;
+              s3 = s3 + ww[e] * g.w;
+            }
+          }
+        }
+      }
+      const float sv[4] = {s0, s1, s2, s3};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float gk = acc[rt][k][r] + cc * sv[r];
+        if (k + 2 <= K - 1) gk = gk - G2[rt][r];
+        G2[rt][r] = G1[rt][r];
+        G1[rt][r] = gk;
+      }
+      if (k > 0 && row < M)
+        *reinterpret_cast<float4*>(nxt + row * kBS + 4 * q) =
+            make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
+    }
+    if (k > 0) __syncthreads();
+  }
+#pragma unroll
+  for (int rt = 0; rt < kRB; ++rt) {
+    const int row = wave * 128 + rt * 16 + jr;
+    if (row < M)
+      *reinterpret_cast<float4*>(A.dh_prev + (int64_t(n) * M + row) * kH + 16 * u + 4 * q) =
+          make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
+  }
+}
+
+inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+}  // namespace
+
+size_t lstm_seq_lds(int M, int K, int64_t nnz) {
+  return size_t(2) * round_up(M, 32) * kQ * 4 + size_t(K) * 2048 * 4 + 512 + size_t(nnz) * 4 +
+         align16(size_t(nnz) * 2);
+}
+
+bool lstm_seq_ok(int M, int H, int K, int64_t nnz) {
+  return H == kH && M >= 1 && M <= kRT * 8 * 32 && K >= 1 && nnz >= 1 &&
+         lstm_seq_lds(M, K, nnz) <= size_t(kLdsBytes - kSeqStaticLds);
+}
+
+size_t lstm_bstep_lds(int M, int K) {
+  return size_t(2) * round_up(M, 16) * kBS * 4 + size_t(K) * 2048 * 4;
+}
+
+bool lstm_bstep_ok(int M, int H, int K) {
+  return H == kH && M >= 1 && M <= kRB * 8 * 16 && K >= 1 && K <= 4 &&
+         lstm_bstep_lds(M, K) <= size_t(kLdsBytes);
+}
+
+int lstm_seq_pairs(int N, int device) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus < 2)
+    cus = 256;
+  const int p = cus / 2;
+  return N < p ? N : p;
+}
+
+hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, const int* rowptr,
+                           const int* col, const float* val, const float* gx, const float* Wh,
+                           const float* bias, const float* h0, const float* c0, float* hs,
+                           float* cs, float* act, float* planes, int64_t pstride, int* flags,
+                           int* status, int P, hipStream_t s) {
+  if (!lstm_seq_ok(M, kH, K, nnz) || N < 1 || T < 1 || P < 1 || P > N)
+    return hipErrorInvalidValue;
+  // the kernel's static LDS (the abort word) counts against the same 160 KB
+  static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_seq),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kLdsBytes - kSeqStaticLds);
+  if (attr != hipSuccess) return attr;
+  int dev = 0, rate_khz = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      rate_khz <= 0)
+    rate_khz = 100000;  // 100 MHz
+  SeqArgs a{rowptr, col, val, M, round_up(M, 32), K, N, T, gates, int(nnz), P,
+            P % 8 == 0 ? 1 : 0, gx, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
+            // a pair hand-off that has not happened after 2 s ends the launch
+            static_cast<unsigned long long>(rate_khz) * 2000ull};
+  hipError_t e = hipMemsetAsync(flags, 0, sizeof(int) * (size_t(2) * P + 1), s);
+  if (e != hipSuccess) return e;
+  // a pair waits for its partner, so every workgroup of the grid must be
+  // resident at once: check the grid against the occupancy query (what a
+  // cooperative launch would check, MI355X_MICROARCH.md §Residency), with one
+  // workgroup per CU of margin, then launch plainly
+  const size_t lds = lstm_seq_lds(M, K, nnz);
+  int per_cu = 0, cus = 0;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_lstm_seq),
+                                                   kST, lds);
+  if (e != hipSuccess) return e;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  if (per_cu < 1 || 2 * P > per_cu * cus) return hipErrorCooperativeLaunchTooLarge;
+  hipLaunchKernelGGL(k_lstm_seq, dim3(2 * P), dim3(kST), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr, const int* tcol,
+                             const float* tval, const float* dh, const float* dh_rec,
+                             const float* dc, const float* act, const float* c_prev,
+                             const float* c_out, const float* Wh, float* dpre, float* dc_prev,
+                             float* dh_prev, hipStream_t s) {
+  if (!lstm_bstep_ok(M, kH, K) || N < 1) return hipErrorInvalidValue;
+  BStepArgs a{trowptr, tcol, tval, M, round_up(M, 16), N, gates, N % 8 == 0 ? 1 : 0, dh, dh_rec,
+              dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev};
+  const size_t lds = lstm_bstep_lds(M, K);
+#define CG_BSTEP(KK)                                                                              \
+  case KK: {                                                                                      \
+    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_bstep<KK>), \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,       \
+                                               kLdsBytes);                                        \
+    if (at != hipSuccess) return at;                                                              \
+    hipLaunchKernelGGL(k_lstm_bstep<KK>, dim3(2 * N), dim3(kST), lds, s, a);                      \
+    break;                                                                                        \
+  }
+  switch (K) {
+    CG_BSTEP(1)
+    CG_BSTEP(2)
+    CG_BSTEP(3)
+    CG_BSTEP(4)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef CG_BSTEP
+  return hipGetLastError();
+}
+
+}  // namespace cg

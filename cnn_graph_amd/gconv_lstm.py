@@ -93,13 +93,20 @@ class GConvLSTMCell:
         self.Wx = torch.nn.Parameter(Wx)
         self.Wh = torch.nn.Parameter(Wh)
         self.b = torch.nn.Parameter(b)
-        # h path of a step: "fused" = cg_lstm_hconv_step (one launch), "unfused"
-        # = chebyshev5 + pointwise kernel; "auto" picks fused where it applies
-        if hconv not in ("auto", "fused", "unfused"):
-            raise ValueError("hconv must be 'auto', 'fused' or 'unfused'")
+        # h path: "seq" = the whole layer's T steps in one launch
+        # (cg_lstm_seq_forward) and one launch per BPTT step (cg_lstm_bwd_step);
+        # "fused" = one launch per forward step (cg_lstm_hconv_step); "unfused"
+        # = chebyshev5 + pointwise kernel; "auto" picks the first that applies
+        if hconv not in ("auto", "seq", "fused", "unfused"):
+            raise ValueError("hconv must be 'auto', 'seq', 'fused' or 'unfused'")
         supported = ops.lstm_hconv_supported(self.plan, H, self._K)
+        seq_ok = ops.lstm_seq_supported(self.plan, H, self._K)
         if hconv == "fused" and not supported:
             raise ValueError(f"hconv='fused' needs H = 32 and M <= 1024 (H={H}, M={self.plan.M})")
+        if hconv == "seq" and not seq_ok:
+            raise ValueError(f"hconv='seq' needs H = 32, M <= 1024, K <= 4 and L~ in LDS "
+                             f"(H={H}, M={self.plan.M}, K={self._K})")
+        self.seq = seq_ok and hconv in ("auto", "seq")
         self.fused = supported and hconv != "unfused"
 
     # -- reference properties ---------------------------------------------------
@@ -177,10 +184,15 @@ class _CellStep(torch.autograd.Function):
         H, K, plan = cell._num_units, cell._K, cell.plan
         dh = dh_out.contiguous() if dh_out is not None else None
         dc = dc_out.contiguous() if dc_out is not None else None
-        dpre, dc_prev = ops.lstm_cell_backward(dh, None, dc, act, c, c_out, H, cell.gates)
+        if cell.fused and cell.seq:  # one launch: gates backward + the h-conv's dh
+            dpre, dc_prev, dh_prev = ops.lstm_bwd_step(plan, dh, None, dc, act, c, c_out, Wh, K,
+                                                       cell.gates)
+        else:
+            dpre, dc_prev = ops.lstm_cell_backward(dh, None, dc, act, c, c_out, H, cell.gates)
         dx, dWx = ops.cheb_backward(plan, dpre, basis_x, Wx, K, need_dx=ctx.needs_input_grad[0])
         if cell.fused:
-            dh_prev, _ = ops.cheb_backward(plan, dpre, None, Wh, K, need_dW=False)
+            if not cell.seq:
+                dh_prev, _ = ops.cheb_backward(plan, dpre, None, Wh, K, need_dW=False)
             dWh = _hweight_grad_planes([h.view(-1, H)], [hb[k] for k in range(K - 1)], [dpre], H, K)
         else:
             dh_prev, dWh = ops.cheb_backward(plan, dpre, hb, Wh, K)
@@ -229,13 +241,17 @@ class _Layer(torch.autograd.Function):
         hs = torch.empty((T, N, M, H), **f32)
         cs = torch.empty((T, N, M, H), **f32)
         act = torch.empty((T, R, 4 * H), **f32)
-        fused = cell.fused
+        fused = cell.fused or cell.seq
         # h bases kept for the backward's weight gradient: the fused h-step
         # writes the orders 1..K-1 as planes [K-1][T][R][H] (order 0 is h_prev)
         planes = torch.empty((max(K - 1, 1), T, R, H), **f32) if fused else None
         basis_h = None if fused else torch.empty((T, R, H * K), **f32)
         gh = None if fused else torch.empty((N, M, 4 * H), **f32)
-        for t in range(T):
+        if cell.seq:  # all T steps in one launch
+            ops.lstm_seq_forward(plan, gx, Wh, b, K, T, N, gates, h0=None if zero_init else h0,
+                                 c0=None if zero_init else c0, out_hs=hs, out_cs=cs, out_act=act,
+                                 planes=planes[0], plane_stride=T * R * H)
+        for t in range(0 if cell.seq else T):
             h_prev = (None if zero_init else h0) if t == 0 else hs[t - 1]
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
             if h_prev is not None and fused:  # one launch: h-conv + gates
@@ -266,6 +282,13 @@ class _Layer(torch.autograd.Function):
         t_first = 1 if zero_init else 0  # first step whose h-conv ran
         for t in range(T - 1, -1, -1):
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
+            if cell.seq and t >= t_first:
+                # one launch: gates backward, dBasis = dpre Wh^T on MFMA and the
+                # reverse recurrence over L~^T -> the gradient of h_{t-1}
+                _, dc, dh_rec = ops.lstm_bwd_step(plan, None if dhs is None else dhs[t], dh_rec,
+                                                  dc, act[t], c_prev, cs[t], Wh, K, gates,
+                                                  out_dpre=dpre[t])
+                continue
             dpre_t, dc = ops.lstm_cell_backward(None if dhs is None else dhs[t], dh_rec, dc, act[t],
                                                 c_prev, cs[t], H, gates, out_dpre=dpre[t])
             if t >= t_first:

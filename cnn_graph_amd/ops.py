@@ -580,6 +580,98 @@ def lstm_cell_backward(dh, dh_rec, dc, act, c, c_out, H: int, gates="reference",
     return dpre, dc_prev
 
 
+def lstm_seq_supported(plan: ChebPlan, H: int, K: int) -> bool:
+    """Whether the one-launch layer forward (cg_lstm_seq_forward) and the
+    one-launch BPTT step (cg_lstm_bwd_step) serve this graph / H / K."""
+    ok = ctypes.c_int32()
+    _lib.call("cg_lstm_seq_supported", plan.handle, int(H), int(K), ctypes.byref(ok))
+    return bool(ok.value)
+
+
+def lstm_seq_forward(plan: ChebPlan, gx, Wh, bias, K: int, T: int, N: int, gates="reference",
+                     h0=None, c0=None, out_hs=None, out_cs=None, out_act=None, planes=None,
+                     plane_stride: int = 0, check: bool = False):
+    """All T steps of a gconv-LSTM layer in ONE launch (cg_lstm_seq_forward):
+    gx [T, N, M, 4H] (the x-conv of every step), h0 / c0 [N, M, H] or None
+    (zero state).  planes (optional; a tensor whose storage holds K-1 planes
+    [T, N, M, H] plane_stride floats apart) receives T_k of h_{t-1}, k >= 1.
+    check=True waits for the stream and raises if a pair hand-off timed out.
+    Returns (hs [T, N, M, H], cs [T, N, M, H], act [T, N, M, 4H] or None)."""
+    _check_dev("gx", gx)
+    H = int(Wh.shape[1]) // 4
+    M = plan.M
+    R = T * N * M
+    if not gx.is_contiguous() or gx.numel() != R * 4 * H:
+        raise ValueError(f"gx must be a contiguous [{T}, {N}, {M}, {4 * H}] tensor")
+    if tuple(Wh.shape) != (K * H, 4 * H) or not Wh.is_contiguous():
+        raise ValueError(f"Wh must be a contiguous [{K * H}, {4 * H}] tensor")
+    dev = gx.device
+    for name, t, n in (("bias", bias, 4 * H), ("h0", h0, N * M * H), ("c0", c0, N * M * H)):
+        if t is not None:
+            _check_dev(name, t)
+            if not t.is_contiguous() or t.numel() != n or t.data_ptr() % 16:
+                raise ValueError(f"{name}: need a contiguous 16-byte aligned tensor of {n} floats")
+    f32 = dict(device=dev, dtype=torch.float32)
+    hs = out_hs if out_hs is not None else torch.empty((T, N, M, H), **f32)
+    cs = out_cs if out_cs is not None else torch.empty((T, N, M, H), **f32)
+    _check_out("hs", hs, (R, H))
+    _check_out("cs", cs, (R, H))
+    if out_act is not None:
+        _check_out("act", out_act, (R, 4 * H))
+    if planes is not None:
+        _check_dev("planes", planes)
+        need = (K - 2) * plane_stride + R * H if K > 1 else 0
+        avail = planes.untyped_storage().nbytes() // 4 - planes.storage_offset()
+        if K > 1 and (plane_stride < R * H or avail < need or planes.data_ptr() % 16
+                      or plane_stride % 4):
+            raise ValueError("planes: storage too small / misaligned for the K-1 planes")
+    nb = ctypes.c_size_t()
+    _lib.call("cg_lstm_seq_workspace_bytes", plan.handle, int(N), ctypes.byref(nb))
+    ws = torch.empty(int(nb.value), device=dev, dtype=torch.uint8)
+    s = _stream(gx)
+    _lib.call("cg_lstm_seq_forward", plan.handle, int(T), int(N), int(H), int(K), LSTM_GATES[gates],
+              _p(gx), _p(Wh), _p(bias), _p(h0), _p(c0), _p(hs), _p(cs), _p(out_act), _p(planes),
+              int(plane_stride), _p(ws), int(nb.value), s)
+    if check:
+        st = ctypes.c_int32()
+        _lib.call("cg_lstm_seq_status", plan.handle, int(N), _p(ws), ctypes.byref(st), s)
+    return hs, cs, out_act
+
+
+def lstm_bwd_step(plan: ChebPlan, dh, dh_rec, dc, act, c_prev, c_out, Wh, K: int,
+                  gates="reference", out_dpre=None, need_dc_prev=True, out_dh_prev=None):
+    """One BPTT step of a gconv-LSTM layer in ONE launch (cg_lstm_bwd_step):
+    dpre = the gradient of the gate pre-activations, dc_prev, and dh_prev =
+    the h-conv's input gradient.  dh / dh_rec / dc / c_prev may be None (= 0).
+    Returns (dpre [..., 4H], dc_prev [..., H] or None, dh_prev [..., H])."""
+    _check_dev("act", act)
+    _check_dev("c_out", c_out)
+    H = int(Wh.shape[1]) // 4
+    R = act.numel() // (4 * H)
+    N = R // plan.M
+    dev = act.device
+    for name, t in (("dh", dh), ("dh_rec", dh_rec), ("dc", dc), ("c_prev", c_prev),
+                    ("c_out", c_out)):
+        if t is not None:
+            _check_dev(name, t)
+            if not t.is_contiguous() or t.numel() != R * H or t.data_ptr() % 16:
+                raise ValueError(f"{name}: bad shape / alignment {tuple(t.shape)}")
+    if not act.is_contiguous() or act.data_ptr() % 16:
+        raise ValueError("act: need a contiguous 16-byte aligned tensor")
+    if tuple(Wh.shape) != (K * H, 4 * H) or not Wh.is_contiguous():
+        raise ValueError(f"Wh must be a contiguous [{K * H}, {4 * H}] tensor")
+    f32 = dict(device=dev, dtype=torch.float32)
+    dpre = out_dpre if out_dpre is not None else torch.empty(tuple(act.shape), **f32)
+    _check_out("dpre", dpre, (R, 4 * H))
+    dc_prev = torch.empty(tuple(c_out.shape), **f32) if need_dc_prev else None
+    dh_prev = out_dh_prev if out_dh_prev is not None else torch.empty(tuple(c_out.shape), **f32)
+    _check_out("dh_prev", dh_prev, (R, H))
+    _lib.call("cg_lstm_bwd_step", plan.handle, int(N), int(H), int(K), LSTM_GATES[gates], _p(dh),
+              _p(dh_rec), _p(dc), _p(act), _p(c_prev), _p(c_out), _p(Wh), _p(dpre), _p(dc_prev),
+              _p(dh_prev), _stream(act))
+    return dpre, dc_prev, dh_prev
+
+
 def adam_update(param, grad, m, v, step: int, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
                 grad_scale=1.0):
     """In-place TF-1.x Adam step on device (lib/graph_model.py:293)."""

@@ -312,6 +312,39 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
                        int64_t plane_stride, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * gconv-LSTM layer, H = 32, M <= 1024 (lib/gconv_lstm.py:609-627 glstm_layer
+ * -> static_rnn over GConvLSTMCell, :77-221):
+ *
+ * cg_lstm_seq_forward: ALL T steps of one layer in ONE cooperative launch
+ * (two workgroups per sample, one per 16 hidden units, exchanging h through a
+ * per-step flag; c kept in registers; L~ and Wh staged in LDS once).
+ *   gx [T][N][M][4H]  the x-conv of every step (chebyshev5 of the [T*N] batch)
+ *   h0, c0 [N][M][H]  initial state, NULL = zero state (step 0 then has no h-conv)
+ *   hs, cs [T][N][M][H] OUT: h_t and c_t;  act [T][N][M][4H] OUT (nullable):
+ *   gate activations z|i|f|o;  planes (nullable): T_k of h_{t-1} for
+ *   k = 1..K-1 at (k-1)*plane_stride + [T][N][M][H] (steps with an h-conv only)
+ *   workspace: cg_lstm_seq_workspace_bytes (step counters + a status word).
+ * cg_lstm_seq_status: waits for the stream, returns CG_ERR_HIP if a pair
+ *   hand-off timed out (the launch then ends early instead of hanging).
+ * cg_lstm_bwd_step: one BPTT step in ONE launch: dpre (the gradient of the
+ *   gate pre-activations, [N][M][4H]), dc_prev and dh_prev = the h-conv's
+ *   input gradient (reverse Chebyshev recurrence over L~^T of dpre Wh^T).
+ *   dh / dh_rec / dc / c_prev nullable (= 0), dc_prev nullable.  K <= 4.
+ * ------------------------------------------------------------------------- */
+int cg_lstm_seq_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* supported);
+int cg_lstm_seq_workspace_bytes(const cg_plan* plan, int32_t N, size_t* bytes);
+int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t K, int32_t gates,
+                        const float* gx, const float* Wh, const float* bias, const float* h0,
+                        const float* c0, float* hs, float* cs, float* act, float* planes,
+                        int64_t plane_stride, void* workspace, size_t ws_bytes, void* stream);
+int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,
+                       void* stream);
+int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,
+                     const float* dh_rec, const float* dc, const float* act, const float* c_prev,
+                     const float* c_out, const float* Wh, float* dpre, float* dc_prev,
+                     float* dh_prev, void* stream);
+
+/* ---------------------------------------------------------------------------
  * perm_data (lib/coarsening.py:219-240) on device:
  *   out[n][i][f] = perm[i] < M_in ? x[n][perm[i]][f] : 0   (fake vertices are 0)
  * x [N][M_in][F], perm [M_out] (int32), out [N][M_out][F].

@@ -105,7 +105,7 @@ def lstm_config(dev, T=12, N=128, Fin=2, H=32, K=3, hconv="auto"):
     torch.cuda.synchronize()
     f = ev_ms(fwd, 3)
     fb = ev_ms(fwdbwd, 3)
-    return {"config": "E", "hconv": "fused" if cell.fused else "unfused",
+    return {"config": "E", "hconv": "seq" if cell.seq else "fused" if cell.fused else "unfused",
             "M": M, "T": T, "N": N, "Fin": Fin, "H": H, "K": K,
             "fwd_ms": round(f, 3), "fwd_bwd_ms": round(fb, 3),
             "samples_per_s": round(N / (fb * 1e-3), 1)}
@@ -164,6 +164,8 @@ def main():
             out = lstm_config(dev)
         elif name == "E_unfused":
             out = lstm_config(dev, hconv="unfused")
+        elif name == "E_step":
+            out = lstm_config(dev, hconv="fused")
         elif name == "R":
             out = resgnn_config(dev)
         else:

@@ -235,14 +235,16 @@ def test_config_E_sequence_path_equals_cell_steps(dev):
 
 
 def test_fused_hstep_equals_unfused(dev):
-    """The one-launch h-step (cg_lstm_hconv_step) against the chebyshev5 +
-    pointwise pair on config E's graph at N = 16 (the 2-workgroups-per-sample
-    XCD pairing): states, every gradient."""
+    """The one-launch layer forward + one-launch BPTT steps (hconv='seq':
+    cg_lstm_seq_forward / cg_lstm_bwd_step) and the one-launch h-step
+    (cg_lstm_hconv_step) against the chebyshev5 + pointwise pair on config E's
+    graph at N = 16 (the 2-workgroups-per-sample XCD pairing): states, every
+    gradient."""
     from cnn_graph_amd.gconv_lstm import layer
     Lt, _, M = graph_E()
     T, N, Fin, H, K = 5, 16, 2, 32, 3
     res = {}
-    for mode in ("fused", "unfused"):
+    for mode in ("seq", "fused", "unfused"):
         cell, _ = make_cell(Lt, Fin, H, K, "reference", dev, seed=41, hconv=mode)
         g = torch.Generator(device=dev)
         g.manual_seed(3)
@@ -255,5 +257,107 @@ def test_fused_hstep_equals_unfused(dev):
         torch.cuda.synchronize()
         res[mode] = [hs.detach(), cT.detach(), xs.grad, c0.grad, h0.grad] + \
             [p.grad for p in cell.parameters()]
-    for a, b in zip(res["fused"], res["unfused"]):
-        assert O.normwise_err(a.cpu().numpy(), b.cpu().numpy().astype(np.float64)) < 1e-5
+    for mode in ("seq", "fused"):
+        for a, b in zip(res[mode], res["unfused"]):
+            assert O.normwise_err(a.cpu().numpy(), b.cpu().numpy().astype(np.float64)) < 1e-5, mode
+    # the h-conv basis is bit-exact in every mode, so the forward states agree
+    # to the contraction's rounding only
+    assert O.normwise_err(res["seq"][0].cpu().numpy(), res["fused"][0].cpu().numpy().astype(np.float64)) < 1e-6
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 4])
+@pytest.mark.parametrize("gates", ["reference", "standard"])
+def test_bwd_step_equals_pointwise_plus_cheb_backward(dev, K, gates):
+    """cg_lstm_bwd_step (gates backward + dBasis on MFMA + reverse recurrence
+    over L~^T in one launch) against lstm_cell_backward + a dx-only
+    chebyshev5 backward: dpre and dc_prev bitwise (the same expressions),
+    dh_prev within 1e-6; every optional input present and absent.  N = 24:
+    XCD pairing on (N % 8 == 0); N = 5: off."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    Lt, _, M = graph_E()
+    plan = ChebPlan(Lt, device=0)
+    H = 32
+    for N in (24, 5):
+        g = torch.Generator(device=dev)
+        g.manual_seed(100 * K + N)
+        rn = lambda *sh: torch.randn(sh, device=dev, generator=g)  # noqa: E731
+        act = torch.cat([torch.tanh(rn(N, M, H)), torch.sigmoid(rn(N, M, 2 * H)),
+                         torch.tanh(rn(N, M, H))], -1).contiguous()
+        c_prev, c_out, dh, dh_rec, dc = (rn(N, M, H) for _ in range(5))
+        Wh = rn(K * H, 4 * H) * 0.1
+        for opt in ((dh, dh_rec, dc, c_prev), (dh, None, None, None), (None, dh_rec, dc, c_prev)):
+            a_dh, a_dhr, a_dc, a_cp = opt
+            dpre, dcp, dhp = ops.lstm_bwd_step(plan, a_dh, a_dhr, a_dc, act, a_cp, c_out, Wh, K, gates)
+            rdpre, rdcp = ops.lstm_cell_backward(a_dh, a_dhr, a_dc, act, a_cp, c_out, H, gates)
+            rdhp, _ = ops.cheb_backward(plan, rdpre.view(N, M, 4 * H), None, Wh, K, need_dW=False)
+            torch.cuda.synchronize()
+            assert torch.equal(dpre, rdpre)
+            assert torch.equal(dcp, rdcp)
+            assert O.normwise_err(dhp.cpu().numpy(), rdhp.cpu().numpy().astype(np.float64)) < 1e-6
+
+
+def test_seq_forward_more_samples_than_pairs(dev):
+    """N = 136 > the 128 workgroup pairs of a 256-CU chip: pairs take a second
+    sample in turn (XCD pairing on).  States and planes equal the per-step
+    one-launch h-step path; no hand-off timed out."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.gconv_lstm import layer
+    Lt, _, M = graph_E()
+    T, N, Fin, H, K = 3, 136, 2, 32, 3
+    res = {}
+    for mode in ("seq", "fused"):
+        cell, _ = make_cell(Lt, Fin, H, K, "reference", dev, seed=43, hconv=mode)
+        g = torch.Generator(device=dev)
+        g.manual_seed(5)
+        xs = torch.randn((T, N, M, Fin), device=dev, generator=g)
+        c0 = torch.randn((N, M, H), device=dev, generator=g) * 0.5
+        h0 = torch.randn((N, M, H), device=dev, generator=g) * 0.5
+        with torch.no_grad():
+            hs, (cT, _) = layer(cell, xs, (c0, h0))
+        res[mode] = (hs, cT)
+        if mode == "seq":  # explicit call with the status check
+            _, gx = ops.cheb_forward(cell.plan, xs.view(T * N, M, Fin), cell.Wx.detach(), K)
+            hs2, cs2, _ = ops.lstm_seq_forward(cell.plan, gx, cell.Wh.detach(), cell.b.detach(), K,
+                                               T, N, "reference", h0=h0, c0=c0, check=True)
+            assert torch.equal(hs2, hs)
+    torch.cuda.synchronize()
+    for a, b in zip(res["seq"], res["fused"]):  # contraction summed in another order
+        assert O.normwise_err(a.cpu().numpy(), b.cpu().numpy().astype(np.float64)) < TOL
+
+
+def test_config_E_full_batch_gradients_vs_oracle(dev):
+    """Config E at full size (M = 1024, T = 12, K = 3, Fin = 2, H = 32,
+    N = 128 per GPU) through the one-launch layer forward and BPTT steps, with
+    a loss that reads 3 samples only (the filter is per-sample independent):
+    every gradient -- dWx, dWh, db over the whole batch, dx of those samples --
+    against the float64 oracle run on the 3 samples (not against cell
+    stepping); dx of every other sample exactly 0."""
+    from cnn_graph_amd.gconv_lstm import layer
+    Lt, _, M = graph_E()
+    T, N, Fin, H, K = 12, 128, 2, 32, 3
+    cell, L = make_cell(Lt, Fin, H, K, "reference", dev, seed=51)
+    assert cell.seq
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    xs = torch.rand((T, N, M, Fin), device=dev, generator=g)
+    sel = [3, 64, 127]
+    gh = torch.zeros((T, N, M, H), device=dev)
+    gsel = torch.randn((T, len(sel), M, H), device=dev, generator=g)
+    gh[:, sel] = gsel
+    xa = xs.clone().requires_grad_()
+    hs, _ = layer(cell, xa)
+    (hs * gh).sum().backward()
+    torch.cuda.synchronize()
+    f64 = lambda a: a.detach().cpu().numpy().astype(np.float64)  # noqa: E731
+    lap = oracle_lap(cell, L)
+    p = params_np(cell)
+    h_ref, _, caches = LO.layer_forward(f64(xs[:, sel]), p, lap, K, H)
+    assert O.normwise_err(f64(hs[:, sel]), h_ref) < TOL
+    dxs, _, _, dWx, dWh, db = LO.layer_backward(f64(gsel), None, caches, p, lap, K, H)
+    for name, got, ref in (("dWx", cell.Wx.grad, dWx), ("dWh", cell.Wh.grad, dWh),
+                           ("db", cell.b.grad, db), ("dx", xa.grad[:, sel], dxs)):
+        err = O.normwise_err(f64(got), ref)
+        assert err < TOL, (name, err)
+    rest = [i for i in range(N) if i not in sel]
+    assert int(torch.count_nonzero(xa.grad[:, rest])) == 0
