@@ -6,7 +6,7 @@ SRC_DIR  := cnn_graph_amd/csrc
 OBJ_DIR  ?= build/obj
 LIB      ?= cnn_graph_amd/libcheb_mi355.so
 SRCS     := $(SRC_DIR)/cheb_fast.hip $(SRC_DIR)/cheb_resident.hip $(SRC_DIR)/cheb_stream.hip $(SRC_DIR)/cheb_wide.hip $(SRC_DIR)/graph_ops.hip \
-            $(SRC_DIR)/lstm.hip $(SRC_DIR)/lstm_fused.hip $(SRC_DIR)/lstm_seq.hip $(SRC_DIR)/epilogue.hip $(SRC_DIR)/fourier.hip \
+            $(SRC_DIR)/lstm.hip $(SRC_DIR)/lstm_fused.hip $(SRC_DIR)/lstm_seq.hip $(SRC_DIR)/cheb_group.hip $(SRC_DIR)/epilogue.hip $(SRC_DIR)/fourier.hip \
             $(SRC_DIR)/cheb_abi.cpp $(SRC_DIR)/comm.cpp $(SRC_DIR)/coarsen.cpp \
             $(SRC_DIR)/lds_layout.cpp
 # fast resident kernels: one object per instantiation of cheb_fast_kern.h

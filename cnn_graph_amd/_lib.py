@@ -19,8 +19,10 @@ CG_PATH_AUTO, CG_PATH_RESIDENT, CG_PATH_STREAM = 0, 1, 2
 CG_ACT_NONE, CG_ACT_RELU, CG_ACT_TANH = 0, 1, 2
 PATHS = {"auto": CG_PATH_AUTO, "resident": CG_PATH_RESIDENT, "stream": CG_PATH_STREAM}
 CG_VARIANT_AUTO, CG_VARIANT_CLASSIC, CG_VARIANT_UNFUSED_DW, CG_VARIANT_NARROW = 0, 1, 2, 3
+CG_VARIANT_STEPS = 4
 VARIANTS = {"auto": CG_VARIANT_AUTO, "classic": CG_VARIANT_CLASSIC,
-            "unfused_dw": CG_VARIANT_UNFUSED_DW, "narrow": CG_VARIANT_NARROW}
+            "unfused_dw": CG_VARIANT_UNFUSED_DW, "narrow": CG_VARIANT_NARROW,
+            "steps": CG_VARIANT_STEPS}
 CG_BASIS_ROWS, CG_BASIS_ORDERS, CG_BASIS_PLANES = 0, 1, 2
 BASIS_LAYOUTS = {"rows": CG_BASIS_ROWS, "orders": CG_BASIS_ORDERS, "planes": CG_BASIS_PLANES}
 

@@ -237,6 +237,24 @@ hipError_t launch_wide_dypass(const float* dy, const float* basis, const float* 
 hipError_t launch_wide_assemble(const float* T, int64_t plane, int N, int M, int Fin, int K,
                                 float* basis, hipStream_t s);
 
+// ---- channel-group resident kernels (cheb_group.hip): M <= 1024, Fin % 8 == 0 ----
+// One workgroup per (sample, 8 channels) runs the whole recurrence in LDS.
+bool grp_ok(int M, int64_t nnz, int Fin, int K, int Fout);
+size_t grp_partial_bytes(int N, int M, int Fin, int Fout);
+// forward, planes basis layout: basis planes [K][N*M][Fin] (plane 0 = x) and,
+// when y != NULL, y = act(basis W + res) via per-group partials yp
+// (grp_partial_bytes of workspace)
+hipError_t launch_grp_fwd(const int* rowptr, const int* col, const float* val, const int* order,
+                          int64_t nnz, int N,
+                          int M, int Fin, int K, int Fout, const float* x, const float* W,
+                          float* basis, float* yp, const float* res, int act, float* y,
+                          hipStream_t s);
+// backward: the whole reverse recurrence from the k-major dBasis planes D; dx (+)= G_0
+hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tval, const int* order,
+                           int64_t nnzT,
+                           int N, int M, int Fin, int K, const float* D, float* dx, int dx_acc,
+                           hipStream_t s);
+
 // C[Mg x Ng] (+)= op(A)[Mg x Kg] * op(B)[Kg x Ng]; fp32 in/out on MFMA f32.
 // trans_a: A stored [Kg][lda] (A^T row-major); trans_b: B stored [Ng][ldb].
 // splits > 1: the K range is cut into `splits` slices, slice s writes
@@ -327,18 +345,18 @@ hipError_t launch_lstm_hstep(int gates, int N, int M, int K, const int* rowptr, 
 // the BPTT step in one launch (lstm_seq.hip).  H == 32, M <= 1024.
 size_t lstm_seq_lds(int M, int K, int64_t nnz);
 bool lstm_seq_ok(int M, int H, int K, int64_t nnz);
-size_t lstm_bstep_lds(int M, int K);
-bool lstm_bstep_ok(int M, int H, int K);
+size_t lstm_bstep_lds(int M, int K, int64_t nnzT);
+bool lstm_bstep_ok(int M, int H, int K, int64_t nnzT);
 // workgroup pairs of the persistent forward (min(N, CUs / 2))
 int lstm_seq_pairs(int N, int device);
 // flags: 2P + 1 ints (pair step counters, then the status word), zeroed here
 hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, const int* rowptr,
-                           const int* col, const float* val, const float* gx, const float* Wh,
+                           const int* col, const float* val, const int* order, const float* gx, const float* Wh,
                            const float* bias, const float* h0, const float* c0, float* hs,
                            float* cs, float* act, float* planes, int64_t pstride, int* flags,
                            int* status, int P, hipStream_t s);
 hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr, const int* tcol,
-                             const float* tval, const float* dh, const float* dh_rec,
+                             const float* tval, const int* order, int64_t nnzT, const float* dh, const float* dh_rec,
                              const float* dc, const float* act, const float* c_prev,
                              const float* c_out, const float* Wh, float* dpre, float* dc_prev,
                              float* dh_prev, hipStream_t s);

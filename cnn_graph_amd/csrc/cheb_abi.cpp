@@ -41,6 +41,11 @@ struct cg_plan {
   // lengths; null when the row lengths are near-uniform
   int* rperm = nullptr;
   int* trperm = nullptr;
+  // rows of L~ / L~^T by decreasing length, always present: the LDS-resident
+  // kernels deal rows to lanes in this order so a wave's rows have (nearly)
+  // equal lengths and its unrolled gather loop has no idle entries
+  int* lorder = nullptr;
+  int* tlorder = nullptr;
   // thread-slot images of L~ and L~^T for the resident kernels (M <= 2048)
   struct Slots {
     int* buf = nullptr;  // one allocation: row | len | beg | col | val | wlen
@@ -260,7 +265,8 @@ int upload(T** dst, const T* src, size_t count) {
 
 void free_plan(cg_plan* p) {
   if (!p) return;
-  void* ptrs[] = {p->rowptr, p->col, p->val, p->trowptr, p->tcol, p->tval, p->rperm, p->trperm};
+  void* ptrs[] = {p->rowptr, p->col, p->val, p->trowptr, p->tcol, p->tval, p->rperm, p->trperm,
+                  p->lorder, p->tlorder};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (p->slots.buf) (void)hipFree(p->slots.buf);
@@ -401,6 +407,13 @@ size_t dw_slab_bytes(int64_t R, int32_t N, int FinK, int Fout, int32_t M = 0) {
   return al256(n * size_t(FinK) * size_t(Fout) * 4);
 }
 
+// Channel-group resident kernels (cheb_group.hip) serve the sample-major
+// streaming path for M <= 1024, Fin % 8 == 0 (forward: planes layout only).
+bool use_group(const cg_plan* p, int32_t Fin, int32_t K, int32_t Fout) {
+  return p->variant != CG_VARIANT_STEPS && p->variant != CG_VARIANT_NARROW &&
+         cg::grp_ok(p->M, std::max(p->nnz, p->nnzT), Fin, K, Fout);
+}
+
 // Workspace layout.  forward: [T_1 .. T_{K-2}] (streaming path only).
 // backward: [dW slabs][dBasis] (dBasis for the streaming path only; the
 // reverse recurrence writes G_k over plane k of it, so it needs no ring).
@@ -416,6 +429,8 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
                       cg::wide_dypass_ok(Fin * K, Fout);
   const size_t slabs = dw_slab_bytes(int64_t(N) * p->M, N, Fin * K, Fout, dypass ? p->M : 0);
   *fwd = (pf == CG_PATH_RESIDENT) ? 0 : w.slots;
+  if (pf != CG_PATH_RESIDENT && use_group(p, Fin, K, Fout))  // per-group partial y (planes layout)
+    *fwd = std::max(*fwd, al256(cg::grp_partial_bytes(N, p->M, Fin, Fout)));
   *bwd = slabs + ((pb == CG_PATH_RESIDENT) ? 0 : w.dA);
   return CG_OK;
 }
@@ -543,18 +558,22 @@ int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz, const int
   if (!rc) rc = upload(&p->trowptr, trp.data(), trp.size());
   if (!rc) rc = upload(&p->tcol, tci.data(), tci.size());
   if (!rc) rc = upload(&p->tval, tv.data(), tv.size());
-  if (!rc && nnz > 0 && p->max_row_nnz > 2 * (nnz / M) + 8) {
-    auto order = [M](const int32_t* rp) {
-      std::vector<int32_t> o(size_t(M), 0);
-      for (int32_t r = 0; r < M; ++r) o[size_t(r)] = r;
-      std::stable_sort(o.begin(), o.end(), [rp](int32_t a, int32_t b) {
-        return rp[a + 1] - rp[a] > rp[b + 1] - rp[b];
-      });
-      return o;
-    };
+  auto order = [M](const int32_t* rp) {
+    std::vector<int32_t> o(size_t(M), 0);
+    for (int32_t r = 0; r < M; ++r) o[size_t(r)] = r;
+    std::stable_sort(o.begin(), o.end(), [rp](int32_t a, int32_t b) {
+      return rp[a + 1] - rp[a] > rp[b + 1] - rp[b];
+    });
+    return o;
+  };
+  if (!rc && M > 0) {
     const std::vector<int32_t> o = order(rowptr), ot = order(trp.data());
-    rc = upload(&p->rperm, o.data(), o.size());
-    if (!rc) rc = upload(&p->trperm, ot.data(), ot.size());
+    rc = upload(&p->lorder, o.data(), o.size());
+    if (!rc) rc = upload(&p->tlorder, ot.data(), ot.size());
+    if (!rc && nnz > 0 && p->max_row_nnz > 2 * (nnz / M) + 8) {
+      rc = upload(&p->rperm, o.data(), o.size());
+      if (!rc) rc = upload(&p->trperm, ot.data(), ot.size());
+    }
   }
   if (!rc && nnz > 0) rc = build_slots(&p->slots, M, rowptr, col, val);
   if (!rc && nnz > 0) rc = build_slots(&p->tslots, M, trp.data(), tci.data(), tv.data());
@@ -585,7 +604,7 @@ int cg_plan_set_path(cg_plan* plan, int path) {
 int cg_plan_set_variant(cg_plan* plan, int variant) {
   if (!plan) return fail(CG_ERR_ARG, "null plan");
   if (variant != CG_VARIANT_AUTO && variant != CG_VARIANT_CLASSIC &&
-      variant != CG_VARIANT_UNFUSED_DW && variant != CG_VARIANT_NARROW)
+      variant != CG_VARIANT_UNFUSED_DW && variant != CG_VARIANT_NARROW && variant != CG_VARIANT_STEPS)
     return fail(CG_ERR_ARG, "bad kernel variant %d", variant);
   plan->variant = variant;
   return ok();
@@ -740,6 +759,15 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                                   M, N, K, s));
     else
       CG_HIP(cg::launch_wide_assemble(slots, int64_t(slot), N, M, Fin, K, basis, s));
+  } else if (layout == CG_BASIS_PLANES && use_group(plan, Fin, K, Fout)) {
+    // channel-group resident kernel: the whole recurrence in LDS per (sample,
+    // 8 channels), planes written once, y from per-group MFMA partials
+    if (y && (!workspace || ws_bytes < cg::grp_partial_bytes(N, M, Fin, Fout)))
+      return fail(CG_ERR_ARG, "forward workspace too small for the group partials");
+    CG_HIP(cg::launch_grp_fwd(plan->rowptr, plan->col, plan->val, plan->lorder, plan->nnz, N, M, Fin, K,
+                              Fout, x,
+                              W, basis, static_cast<float*>(workspace), res, act, y, s));
+    return ok();
   } else if (layout == CG_BASIS_PLANES) {
     // planes layout: T_k IS plane k of the basis (plane 0 a copy of x), every
     // step writes its own plane, no assembly step (lib/graph_conv.py:159-169)
@@ -912,6 +940,11 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
                                       (k + 2 <= K - 1) ? G(k + 2) : nullptr, G(k), G(k), M, B, 2,
                                       k >= 1 ? 2.f : 1.f, s));
         CG_HIP(cg::launch_vm_to_sm(G(0), N, int64_t(M) * Fin, dx, dx_acc, s));
+      } else if (use_group(plan, Fin, K, Fout)) {
+        // the whole reverse recurrence in LDS per (sample, 8 channels)
+        CG_HIP(cg::launch_grp_clen(plan->trowptr, plan->tcol, plan->tval, plan->tlorder, plan->nnzT, N,
+                                   M, Fin, K,
+                                   dA, dx, dx_acc, s));
       } else {
         const int* rperm = (Fin >= 16) ? plan->trperm : nullptr;
         auto G = [&](int k) { return dA + size_t(k) * slot; };
@@ -1410,7 +1443,8 @@ static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) =
 
 int cg_lstm_seq_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* supported) {
   if (!plan || !supported) return fail(CG_ERR_ARG, "lstm_seq_supported: null argument");
-  *supported = (cg::lstm_seq_ok(plan->M, H, K, plan->nnz) && cg::lstm_bstep_ok(plan->M, H, K)) ? 1 : 0;
+  *supported =
+      (cg::lstm_seq_ok(plan->M, H, K, plan->nnz) && cg::lstm_bstep_ok(plan->M, H, K, plan->nnzT)) ? 1 : 0;
   return ok();
 }
 
@@ -1453,7 +1487,7 @@ int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t 
   const int P = cg::lstm_seq_pairs(N, plan->device);
   int* flags = static_cast<int*>(workspace);
   CG_HIP(cg::launch_lstm_seq(gates, T, N, plan->M, K, plan->nnz, plan->rowptr, plan->col, plan->val,
-                             gx, Wh, bias, h0, c0, hs, cs, act, planes, plane_stride, flags,
+                             plan->lorder, gx, Wh, bias, h0, c0, hs, cs, act, planes, plane_stride, flags,
                              flags + 2 * P, P, reinterpret_cast<hipStream_t>(stream)));
   return ok();
 }
@@ -1481,7 +1515,7 @@ int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gat
   if (!plan || N < 1 || K < 1) return fail(CG_ERR_ARG, "lstm_bwd_step: bad plan / N / K");
   if (!act || !c_out || !Wh || !dpre || !dh_prev)
     return fail(CG_ERR_ARG, "lstm_bwd_step: null act / c_out / Wh / dpre / dh_prev");
-  if (!cg::lstm_bstep_ok(plan->M, H, K))
+  if (!cg::lstm_bstep_ok(plan->M, H, K, plan->nnzT))
     return fail(CG_ERR_UNSUPPORTED, "lstm_bwd_step: needs H = 32, M <= 1024, K <= 4 (M=%d H=%d K=%d)",
                 plan->M, H, K);
   const void* all[] = {dh, dh_rec, dc, act, c_prev, c_out, dpre, dc_prev, dh_prev};
@@ -1493,7 +1527,8 @@ int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gat
     for (const void* i : ins)
       if (o && o == i) return fail(CG_ERR_ARG, "lstm_bwd_step: outputs must not alias inputs");
   if ((rc = check_device(plan))) return rc;
-  CG_HIP(cg::launch_lstm_bstep(gates, N, plan->M, K, plan->trowptr, plan->tcol, plan->tval, dh, dh_rec,
+  CG_HIP(cg::launch_lstm_bstep(gates, N, plan->M, K, plan->trowptr, plan->tcol, plan->tval,
+                               plan->tlorder, plan->nnzT, dh, dh_rec,
                                dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev,
                                reinterpret_cast<hipStream_t>(stream)));
   return ok();

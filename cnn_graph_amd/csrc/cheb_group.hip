@@ -1,0 +1,401 @@
+// Channel-group resident kernels for mid-size graphs with many input channels
+// (M <= 1024, Fin a multiple of 8): the ResGNN hidden layers of the humanflow
+// model (config R: M = 1024, Fin = Fout = 32, K = 20; lib/graph_conv.py:234-330)
+// and the h-conv-sized filters of the gconv-LSTM.  On the streaming path each
+// Chebyshev step is its own launch (K - 1 of them per filter, ~11 us each, and
+// the y row GEMM re-reads the whole K-plane basis); here ONE workgroup owns one
+// sample x 8 channels and runs the whole recurrence out of LDS:
+//
+// k_grp_fwd   T_0 = x (its 8 channels), T_{k+1} = 2 L~ T_k - T_{k-1} (CSR order
+//             from +0, contraction off: the basis is bit-exact to
+//             lib/graph.py::chebyshev), every T_k written ONCE as its slice of
+//             basis plane k (the planes layout [K][N*M][Fin]); the contraction
+//             y_g = sum_k T_k W_k over the group's 8 channels on
+//             v_mfma_f32_32x32x2_f32, transposed (y^T = W^T T^T) so the B
+//             operand is the lane's own T_k straight from the SpMM; the
+//             per-group partial y_g leaves once per filter.
+// k_grp_yred  y = act(sum_g y_g + res), groups added in a fixed order.
+// k_grp_clen  the backward's reverse recurrence G_{K-1} = D_{K-1},
+//             G_k = (D_k + c L~^T G_{k+1}) - G_{k+2} (c = 2; 1 at k = 0) over the
+//             explicit L~^T with G in LDS, D_k streamed from the k-major dBasis
+//             planes; dx (+)= G_0.  Same expressions and order as
+//             cheb_stream.hip::k_clenshaw_step, so dx is bitwise the same.
+//
+// Geometry: 512 threads (8 waves, two per SIMD, 256 registers per lane); lane
+// (row j of a 32-row tile, half hh) owns channels 4hh .. 4hh+3 of the group for
+// four row tiles (rows order[(wave + 8 rt) * 32 + j], the rows dealt by
+// decreasing length so each tile's unrolled gather loop -- lds_spmm.h -- is
+// as long as its longest row).  LDS: two [M][8] slots (T_k /
+// T_{k+1} or G_{k+1} / G_k), the CSR (16-bit columns + values), and for the
+// forward the group's rows of W as MFMA A operands.  The groups of a sample sit
+// on one XCD (blocks b, b + 8, .. under round-robin placement) so their 32-byte
+// slices of each basis row merge in one L2.
+#include "cg_internal.h"
+#include "lds_spmm.h"
+
+namespace cg {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kGT = 512;  // threads per workgroup
+constexpr int kGQ = 8;    // channels per group
+constexpr int kGRT = 4;   // 32-row tiles per wave (8 waves x 4 x 32 = 1024 rows)
+
+inline int rup(int v, int m) { return (v + m - 1) / m * m; }
+
+// block -> (sample, group): the G groups of a sample on one XCD
+__device__ __forceinline__ void grp_map(int b, int G, int& n, int& g) {
+  const int per = 8 * G;  // 8 samples x G groups per block of 8*G workgroups
+  const int blk = b / per, rem = b - blk * per;
+  g = rem >> 3;
+  n = blk * 8 + (rem & 7);
+}
+
+struct GrpFwdArgs {
+  const int* rowptr;
+  const int* col;
+  const float* val;
+  const int* order;  // rows by decreasing length (lane -> row)
+  int M, Mr, Fin, K, Fout, N, nnz, G;
+  const float* x;   // [N][M][Fin]
+  const float* W;   // [Fin*K][Fout], row fin*K + k
+  float* basis;     // planes [K][N*M][Fin]
+  int64_t plane;    // N*M*Fin
+  float* yp;        // [G][N*M][Fout] partial y per group, or NULL (basis only)
+};
+
+template <int NOT>  // 32-wide output tiles (Fout <= 32 * NOT)
+__global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  int n, g;
+  grp_map(blockIdx.x, A.G, n, g);
+  if (n >= A.N) return;  // grid padded to whole XCD rounds (uniform per workgroup)
+  const int M = A.M, K = A.K, Fin = A.Fin, Fout = A.Fout;
+  float* slot0 = smem;
+  float* slot1 = smem + A.Mr * kGQ;
+  float* s_W = slot1 + A.Mr * kGQ;  // [K][s 4][hh 2][NOT][i 32]
+  float* s_val = s_W + K * 256 * NOT;
+  unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
+  const bool want_y = A.yp != nullptr;
+  if (want_y) {
+    for (int e = tid; e < K * 256 * NOT; e += kGT) {
+      const int i = e & 31, ot = (e >> 5) % NOT, h2 = (e / (32 * NOT)) & 1;
+      const int s = (e / (64 * NOT)) & 3, k = e / (256 * NOT);
+      const int ch = kGQ * g + 4 * h2 + s, out = ot * 32 + i;
+      s_W[e] = out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
+    }
+  }
+  for (int e = tid; e < A.nnz; e += kGT) {
+    s_val[e] = A.val[e];
+    s_col[e] = static_cast<unsigned short>(A.col[e]);
+  }
+  if (tid < 2 * kGQ) (tid < kGQ ? slot0 : slot1)[M * kGQ + (tid & (kGQ - 1))] = 0.f;  // zero row M
+  int row[kGRT], rb[kGRT], re[kGRT], wl[kGRT];
+  bool rv[kGRT];
+  float Tc[kGRT][4];
+  const int c0 = kGQ * g + 4 * hh;
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    const int idx = (wave + 8 * rt) * 32 + j;
+    rv[rt] = idx < M;
+    row[rt] = rv[rt] ? A.order[idx] : M;
+    rb[rt] = rv[rt] ? A.rowptr[row[rt]] : 0;
+    re[rt] = rv[rt] ? A.rowptr[row[rt] + 1] : 0;
+    wl[rt] = wave_max(re[rt] - rb[rt]);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rv[rt]) {
+      const int64_t o = (int64_t(n) * M + row[rt]) * Fin + c0;
+      v = *reinterpret_cast<const float4*>(A.x + o);
+      *reinterpret_cast<float4*>(A.basis + o) = v;  // plane 0 = x
+      *reinterpret_cast<float4*>(slot0 + row[rt] * kGQ + 4 * hh) = v;
+    }
+    Tc[rt][0] = v.x;
+    Tc[rt][1] = v.y;
+    Tc[rt][2] = v.z;
+    Tc[rt][3] = v.w;
+  }
+  f32x16 acc[kGRT][NOT];
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[rt][ot][e] = 0.f;
+  __syncthreads();
+  for (int k = 0; k < K; ++k) {
+    if (want_y) {
+      // y^T[out][row] += W_k^T[out][ch] T_k^T[ch][row], channels 4hh + s
+      const float* wk = s_W + k * 256 * NOT + hh * 32 * NOT + j;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) {
+          const float a = wk[s * 64 * NOT + ot * 32];
+#pragma unroll
+          for (int rt = 0; rt < kGRT; ++rt)
+            acc[rt][ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Tc[rt][s], acc[rt][ot], 0, 0, 0);
+        }
+    }
+    if (k + 1 < K) {
+      const float* cur = (k & 1) ? slot1 : slot0;
+      float* nxt = (k & 1) ? slot0 : slot1;
+      float* pl = A.basis + int64_t(k + 1) * A.plane;
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt) {
+        if (!rv[rt]) continue;
+        float4 sm;
+        with_row_len(wl[rt], [&](auto lc) {
+          sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+        });
+        float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
+        float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kGQ + 4 * hh);
+        if (k >= 1) {  // T_{k-1}: the slot entry being overwritten
+          const float4 p = *own;
+          s0 = 2.f * s0 - p.x;
+          s1 = 2.f * s1 - p.y;
+          s2 = 2.f * s2 - p.z;
+          s3 = 2.f * s3 - p.w;
+        }
+        const float4 o = make_float4(s0, s1, s2, s3);
+        *own = o;
+        *reinterpret_cast<float4*>(pl + (int64_t(n) * M + row[rt]) * Fin + c0) = o;
+        Tc[rt][0] = s0;
+        Tc[rt][1] = s1;
+        Tc[rt][2] = s2;
+        Tc[rt][3] = s3;
+      }
+      __syncthreads();
+    }
+  }
+  if (!want_y) return;
+  // lane (row, hh) holds outputs ot*32 + 8q + 4hh + m (q = e / 4, m = e % 4)
+  float* yg = A.yp + int64_t(g) * A.N * M * Fout;
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    if (!rv[rt]) continue;
+    float* yr = yg + (int64_t(n) * M + row[rt]) * Fout;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int o0 = ot * 32 + 8 * q + 4 * hh;
+        if (o0 + 4 <= Fout && (Fout & 3) == 0) {
+          *reinterpret_cast<float4*>(yr + o0) =
+              make_float4(acc[rt][ot][4 * q], acc[rt][ot][4 * q + 1], acc[rt][ot][4 * q + 2],
+                          acc[rt][ot][4 * q + 3]);
+        } else {
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            if (o0 + m < Fout) yr[o0 + m] = acc[rt][ot][4 * q + m];
+        }
+      }
+  }
+}
+
+// y = act(sum_g yp[g] + res), groups added in order (bitwise reproducible)
+__global__ __launch_bounds__(256) void k_grp_yred(const float* __restrict__ yp, int G, int64_t n,
+                                                  const float* __restrict__ res, int act,
+                                                  float* __restrict__ y) {
+#pragma clang fp contract(off)
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    float s = yp[i];
+    for (int gg = 1; gg < G; ++gg) s = s + yp[int64_t(gg) * n + i];
+    if (res) s = s + res[i];
+    if (act == 1) s = s > 0.f ? s : 0.f;
+    y[i] = s;
+  }
+}
+
+struct GrpClenArgs {
+  const int* trowptr;  // L~^T
+  const int* tcol;
+  const float* tval;
+  const int* order;    // rows of L~^T by decreasing length (lane -> row)
+  int M, Mr, Fin, K, N, nnz, G;
+  const float* D;  // k-major dBasis planes [K][N*M][Fin]
+  int64_t plane;   // N*M*Fin
+  float* dx;       // [N][M][Fin]
+  int dx_acc;
+};
+
+__global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  int n, g;
+  grp_map(blockIdx.x, A.G, n, g);
+  if (n >= A.N) return;
+  const int M = A.M, K = A.K, Fin = A.Fin;
+  float* slotA = smem;
+  float* slotB = smem + A.Mr * kGQ;
+  float* s_val = slotB + A.Mr * kGQ;
+  unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
+  for (int e = tid; e < A.nnz; e += kGT) {
+    s_val[e] = A.tval[e];
+    s_col[e] = static_cast<unsigned short>(A.tcol[e]);
+  }
+  int row[kGRT], rb[kGRT], re[kGRT], wl[kGRT];
+  bool rv[kGRT];
+  int64_t off[kGRT];
+  if (tid < 2 * kGQ) (tid < kGQ ? slotA : slotB)[M * kGQ + (tid & (kGQ - 1))] = 0.f;  // zero row M
+  const int c0 = kGQ * g + 4 * hh;
+  float G1[kGRT][4], G2[kGRT][4], Dn[kGRT][4];
+  auto loadD = [&](int k) {
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rv[rt]) v = *reinterpret_cast<const float4*>(A.D + int64_t(k) * A.plane + off[rt]);
+      Dn[rt][0] = v.x;
+      Dn[rt][1] = v.y;
+      Dn[rt][2] = v.z;
+      Dn[rt][3] = v.w;
+    }
+  };
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    const int idx = (wave + 8 * rt) * 32 + j;
+    rv[rt] = idx < M;
+    row[rt] = rv[rt] ? A.order[idx] : M;
+    rb[rt] = rv[rt] ? A.trowptr[row[rt]] : 0;
+    re[rt] = rv[rt] ? A.trowptr[row[rt] + 1] : 0;
+    off[rt] = (int64_t(n) * M + (rv[rt] ? row[rt] : 0)) * Fin + c0;
+    wl[rt] = wave_max(re[rt] - rb[rt]);
+  }
+  loadD(K - 1);
+  // G_{K-1} = D_{K-1} + c * (+0)  (k_clenshaw_step's expression with no G_K)
+  const float cl = (K - 1 >= 1) ? 2.f : 1.f;
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      G1[rt][m] = Dn[rt][m] + cl * 0.f;
+      G2[rt][m] = 0.f;
+    }
+  if (K > 1) {
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt)
+      if (rv[rt])
+        *reinterpret_cast<float4*>(slotA + row[rt] * kGQ + 4 * hh) =
+            make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
+    loadD(K - 2);
+  }
+  __syncthreads();
+  for (int k = K - 2; k >= 0; --k) {
+    const float* cur = ((K - 2 - k) & 1) ? slotB : slotA;
+    float* nxt = ((K - 2 - k) & 1) ? slotA : slotB;
+    const float c = k >= 1 ? 2.f : 1.f;
+    float Dk[kGRT][4];
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) Dk[rt][m] = Dn[rt][m];
+    if (k >= 1) loadD(k - 1);  // in flight during this step's gathers
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt) {
+      float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rv[rt])
+        with_row_len(wl[rt], [&](auto lc) {
+          sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+        });
+      const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        float o = Dk[rt][m] + c * sv[m];
+        if (k + 2 <= K - 1) o = o - G2[rt][m];
+        G2[rt][m] = G1[rt][m];
+        G1[rt][m] = o;
+      }
+      if (k > 0 && rv[rt])
+        *reinterpret_cast<float4*>(nxt + row[rt] * kGQ + 4 * hh) =
+            make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
+    }
+    if (k > 0) __syncthreads();
+  }
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    if (!rv[rt]) continue;
+    float4* d = reinterpret_cast<float4*>(A.dx + off[rt]);
+    float4 o = make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
+    if (A.dx_acc) {
+      const float4 p = *d;
+      o = make_float4(p.x + o.x, p.y + o.y, p.z + o.z, p.w + o.w);
+    }
+    *d = o;
+  }
+}
+
+}  // namespace
+
+size_t grp_fwd_lds(int M, int K, int Fout, int64_t nnz) {
+  const int NOT = Fout <= 32 ? 1 : 2;
+  return size_t(2) * rup(M + 1, 32) * kGQ * 4 + size_t(K) * 256 * NOT * 4 + size_t(nnz) * 4 +
+         align16(size_t(nnz) * 2);
+}
+
+size_t grp_clen_lds(int M, int64_t nnzT) {
+  return size_t(2) * rup(M + 1, 32) * kGQ * 4 + size_t(nnzT) * 4 + align16(size_t(nnzT) * 2);
+}
+
+bool grp_ok(int M, int64_t nnz, int Fin, int K, int Fout) {
+  return M >= 1 && M <= kGRT * 8 * 32 && nnz >= 1 && Fin % kGQ == 0 && Fin >= kGQ && K >= 2 &&
+         Fout >= 1 && Fout <= 64 && grp_fwd_lds(M, K, Fout, nnz) <= size_t(kLdsBytes) &&
+         grp_clen_lds(M, nnz) <= size_t(kLdsBytes);
+}
+
+size_t grp_partial_bytes(int N, int M, int Fin, int Fout) {
+  return size_t(Fin / kGQ) * size_t(N) * size_t(M) * size_t(Fout) * 4;
+}
+
+static int grp_grid(int N, int G) { return rup(N, 8) * G; }
+
+hipError_t launch_grp_fwd(const int* rowptr, const int* col, const float* val, const int* order,
+                          int64_t nnz, int N,
+                          int M, int Fin, int K, int Fout, const float* x, const float* W,
+                          float* basis, float* yp, const float* res, int act, float* y,
+                          hipStream_t s) {
+  if (!grp_ok(M, nnz, Fin, K, Fout)) return hipErrorInvalidValue;
+  const int G = Fin / kGQ;
+  GrpFwdArgs a{rowptr, col, val, order, M, rup(M + 1, 32), Fin, K, Fout, N, int(nnz), G, x, W, basis,
+               int64_t(N) * M * Fin, y ? yp : nullptr};
+  const size_t lds = grp_fwd_lds(M, K, Fout, nnz);
+  if (Fout <= 32) {
+    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_fwd<1>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (at != hipSuccess) return at;
+    hipLaunchKernelGGL(k_grp_fwd<1>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+  } else {
+    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_fwd<2>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (at != hipSuccess) return at;
+    hipLaunchKernelGGL(k_grp_fwd<2>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !y) return e;
+  const int64_t n = int64_t(N) * M * Fout;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(k_grp_yred, dim3(unsigned(blocks)), dim3(256), 0, s, yp, G, n, res, act, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tval, const int* order,
+                           int64_t nnzT,
+                           int N, int M, int Fin, int K, const float* D, float* dx, int dx_acc,
+                           hipStream_t s) {
+  if (M > kGRT * 8 * 32 || Fin % kGQ || K < 1 || grp_clen_lds(M, nnzT) > size_t(kLdsBytes))
+    return hipErrorInvalidValue;
+  const int G = Fin / kGQ;
+  GrpClenArgs a{trowptr, tcol, tval, order, M, rup(M + 1, 32), Fin, K, N, int(nnzT), G, D,
+                int64_t(N) * M * Fin, dx, dx_acc};
+  static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+  if (at != hipSuccess) return at;
+  hipLaunchKernelGGL(k_grp_clen, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
+  return hipGetLastError();
+}
+
+}  // namespace cg

@@ -22,6 +22,9 @@
 // the basis is bit-identical to the resident path and to lib/graph.py::chebyshev.
 #include "cg_internal.h"
 
+#include <algorithm>
+#include <type_traits>
+
 namespace cg {
 namespace {
 
@@ -549,67 +552,137 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int Mg, int Ng, int Kg, const 
 
 // dW partial slabs: slab[z][j][f] = sum_{r in chunk z} basis[r][j] * dy[r][f]
 // over the R = N*M basis rows (j < FinK, f < Fout): a skinny TN GEMM whose
-// inner dimension is the whole batch.  Block (z, tile) = 4 waves; wave w
-// streams rows r0 + 2u + h of its quarter of chunk z (lane half h takes the
-// odd rows) straight into v_mfma_f32_32x32x2_f32 (K = 2 rows per MFMA):
-// A lane (j, h) = basis[r][j], B lane (f, h) = dy[r][f] -- each wave load
-// instruction reads two whole 4*FinK / 4*Fout-byte rows.  16 loads per lane
-// are in flight per batch; the 4 wave partials are added in a fixed order
-// through LDS, so the result is bitwise reproducible.  HBM-bound: it reads
-// basis + dy once (4*R*(FinK + Fout) bytes) and is meant to run on a side
-// stream concurrently with the latency-bound backward recurrence.
+// inner dimension is the whole batch.  Block (z, g) = 4 waves owns chunk z and
+// a group of up to 16 of the 32x32 (j, f) output tiles (all of them when
+// FinK/32 * Fout/32 <= 16), so every basis and dy row of the chunk is read
+// from HBM ONCE per group (the earlier one-tile-per-block grid read the basis
+// Fout/32 times and dy FinK/32 times: 3x the compulsory bytes on config D,
+// r03 PMC).  The chunk's rows stream through LDS in batches of 16 (the next
+// batch's 16-B loads are in flight in registers while the 4 waves run the
+// current one); wave w accumulates tiles w, w+4, .. of the group on
+// v_mfma_f32_32x32x2_f32 (K = 2 rows per MFMA: lane half h takes the odd
+// rows), one tile per accumulator, rows in order -- bitwise reproducible.
 // pl_fin > 0: the basis is in the planes layout (column jj = k*pl_fin + fin of
 // row r at basis[k*pl_stride + r*pl_fin + fin]); the slab keeps the rows
 // layout's column order fin*K + k.
+constexpr int kDwRB = 16;     // rows per LDS batch (4 per wave)
+constexpr int kDwTiles = 16;  // output tiles per block at most (4 per wave)
+constexpr int kDwNA = 2;      // basis pieces per lane and staged row (64 lanes x VW floats each)
+// dy pieces per lane and staged row: Fout <= 256 either way
+template <int VW> constexpr int dw_nb() { return VW == 4 ? 1 : 4; }
+
+template <int VW>  // 4: float4 pieces (FinK, Fout, pl_fin multiples of 4), 1: floats
 __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basis,
                                                   const float* __restrict__ dy, int64_t R,
                                                   int FinK, int Fout, int64_t rows_per_chunk,
                                                   float* __restrict__ slab, int pl_fin,
-                                                  int64_t pl_stride, int K) {
-  __shared__ float part[4][32][33];
+                                                  int64_t pl_stride, int K, int tpb) {
+  typedef typename std::conditional<VW == 4, float4, float>::type V;
+  constexpr int kDwNB = dw_nb<VW>();
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = lane >> 5, li = lane & 31;
   const int ftl = (Fout + 31) >> 5;
-  const int jt = blockIdx.y / ftl, ft = blockIdx.y - jt * ftl;
-  const int j = jt * 32 + li, f = ft * 32 + li;
-  const bool jv = j < FinK, fv = f < Fout;
-  const int jc = jv ? j : FinK - 1, fc = fv ? f : Fout - 1;
-  // column jc of row rr at bcol + rr * bld
-  const float* bcol = pl_fin > 0 ? basis + int64_t(jc / pl_fin) * pl_stride + jc % pl_fin : basis + jc;
-  const int64_t bld = pl_fin > 0 ? pl_fin : FinK;
+  const int ntiles = ((FinK + 31) >> 5) * ftl;
+  const int t0 = blockIdx.y * tpb;
+  const int t1 = (t0 + tpb < ntiles) ? t0 + tpb : ntiles;
+  // the group's basis columns [jlo, jhi) (tiles are jt-major) and all of dy
+  const int jlo = (t0 / ftl) * 32;
+  const int jhi0 = ((t1 - 1) / ftl + 1) * 32;
+  const int jhi = jhi0 < FinK ? jhi0 : FinK;
+  const int SA = ((jhi0 - jlo) | 1);         // LDS row strides (odd: the two half-wave
+  const int SB = (((Fout + 31) & ~31) | 1);  // rows of an operand read hit other banks)
+  float* s_a = sm;               // [kDwRB][SA]
+  float* s_b = sm + kDwRB * SA;  // [kDwRB][SB]
   const int64_t c0 = int64_t(blockIdx.x) * rows_per_chunk;
   const int64_t c1 = (c0 + rows_per_chunk < R) ? c0 + rows_per_chunk : R;
-  const int64_t q = (((c1 - c0) + 3) / 4 + 1) & ~int64_t(1);  // even rows per wave
-  const int64_t r0 = c0 + w * q;
-  const int64_t r1 = (r0 + q < c1) ? r0 + q : c1;
-  f32x16 acc;
+  for (int e = threadIdx.x; e < kDwRB * SA; e += 256) s_a[e] = 0.f;  // padding columns
+  for (int e = threadIdx.x; e < kDwRB * SB; e += 256) s_b[e] = 0.f;
+  // this lane's pieces of a staged row: basis columns jlo + VW*(lane + 64 i),
+  // dy columns VW*(lane + 64 i); their offsets from the row's base
+  int64_t aoff[kDwNA];
+  bool av[kDwNA], bv[kDwNB];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  for (int64_t rb = r0; rb < r1; rb += 16) {
-    float a[8], b[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      int64_t rr = rb + 2 * u + h;
-      rr = rr < R ? rr : R - 1;
-      a[u] = bcol[rr * bld];
-      b[u] = dy[rr * Fout + fc];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool rv = (rb + 2 * u + h) < r1;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32((rv && jv) ? a[u] : 0.f, (rv && fv) ? b[u] : 0.f,
-                                                 acc, 0, 0, 0);
-    }
+  for (int i = 0; i < kDwNA; ++i) {
+    const int cc = jlo + VW * (lane + 64 * i);
+    av[i] = cc < jhi;
+    aoff[i] = pl_fin > 0 ? int64_t(cc / pl_fin) * pl_stride + cc % pl_fin : cc;
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r) part[w][(r & 3) + 8 * (r >> 2) + 4 * h][li] = acc[r];
-  __syncthreads();
-  for (int e = threadIdx.x; e < 1024; e += 256) {
-    const int row = e >> 5, col = e & 31;
-    const float s = ((part[0][row][col] + part[1][row][col]) + part[2][row][col]) + part[3][row][col];
-    const int jj = jt * 32 + row, ff = ft * 32 + col;
-    const int jo = pl_fin > 0 ? (jj % pl_fin) * K + jj / pl_fin : jj;
-    if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jo) * Fout + ff] = s;
+  for (int i = 0; i < kDwNB; ++i) bv[i] = VW * (lane + 64 * i) < Fout;
+  const int64_t ald = pl_fin > 0 ? pl_fin : FinK;  // basis row stride
+  V ra[4][kDwNA], rbv[4][kDwNB];
+  auto fetch = [&](int64_t rb) {  // rows rb + 4w .. rb + 4w + 3 into registers
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t rr = rb + 4 * w + q;
+      const bool rv = rr < c1;
+#pragma unroll
+      for (int i = 0; i < kDwNA; ++i)
+        if (av[i]) ra[q][i] = rv ? *reinterpret_cast<const V*>(basis + rr * ald + aoff[i]) : V{};
+#pragma unroll
+      for (int i = 0; i < kDwNB; ++i)
+        if (bv[i]) rbv[q][i] = rv ? *reinterpret_cast<const V*>(dy + rr * Fout + VW * (lane + 64 * i)) : V{};
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float* da = s_a + (4 * w + q) * SA;
+      float* db = s_b + (4 * w + q) * SB;
+#pragma unroll
+      for (int i = 0; i < kDwNA; ++i)
+        if (av[i]) {
+          const float* v = reinterpret_cast<const float*>(&ra[q][i]);
+#pragma unroll
+          for (int c = 0; c < VW; ++c) da[VW * (lane + 64 * i) + c] = v[c];
+        }
+#pragma unroll
+      for (int i = 0; i < kDwNB; ++i)
+        if (bv[i]) {
+          const float* v = reinterpret_cast<const float*>(&rbv[q][i]);
+#pragma unroll
+          for (int c = 0; c < VW; ++c) db[VW * (lane + 64 * i) + c] = v[c];
+        }
+    }
+  };
+  f32x16 acc[kDwTiles / 4];
+#pragma unroll
+  for (int a = 0; a < kDwTiles / 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+  __syncthreads();  // padding zeroed before the first stage
+  if (c0 < c1) fetch(c0);
+  for (int64_t rb = c0; rb < c1; rb += kDwRB) {
+    stage();
+    __syncthreads();
+    if (rb + kDwRB < c1) fetch(rb + kDwRB);  // in flight during the MFMAs
+#pragma unroll
+    for (int a = 0; a < kDwTiles / 4; ++a) {
+      const int t = t0 + w + 4 * a;
+      if (t < t1) {
+        const int jt = t / ftl, ft = t - jt * ftl;
+        const float* pa = s_a + h * SA + (jt * 32 - jlo) + li;
+        const float* pb = s_b + h * SB + ft * 32 + li;
+#pragma unroll
+        for (int u = 0; u < kDwRB / 2; ++u)
+          acc[a] = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[2 * u * SA], pb[2 * u * SB], acc[a], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // the batch buffers are restaged next
+  }
+#pragma unroll
+  for (int a = 0; a < kDwTiles / 4; ++a) {
+    const int t = t0 + w + 4 * a;
+    if (t >= t1) continue;
+    const int jt = t / ftl, ft = t - jt * ftl;
+    const int ff = ft * 32 + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jj = jt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int jo = pl_fin > 0 ? (jj % pl_fin) * K + jj / pl_fin : jj;
+      if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jo) * Fout + ff] = acc[a][r];
+    }
   }
 }
 
@@ -804,9 +877,34 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
                            float* slab, hipStream_t s, int pl_fin, int64_t pl_stride, int K) {
   const int chunks = dw_chunks(R);
   const int64_t rpc = (R + chunks - 1) / chunks;
-  const dim3 grid(chunks, ((FinK + 31) / 32) * ((Fout + 31) / 32));
-  hipLaunchKernelGGL(k_dw_slabs, grid, dim3(256), 0, s, basis, dy, R, FinK, Fout, rpc, slab,
-                     pl_fin, pl_stride, K);
+  const int jtl = (FinK + 31) / 32, ftl = (Fout + 31) / 32;
+  const int ntiles = jtl * ftl;
+  const int vw = (FinK % 4 == 0 && Fout % 4 == 0 && (pl_fin == 0 || pl_fin % 4 == 0)) ? 4 : 1;
+  if (Fout > 256) return hipErrorInvalidValue;
+  // tiles per block: as many as the staging pieces allow (every group
+  // re-reads the chunk's dy rows and its own basis columns)
+  int tpb = kDwTiles, groups = 0, span = 0;
+  for (;; tpb /= 2) {
+    groups = (ntiles + tpb - 1) / tpb;
+    span = 0;
+    bool ok = true;
+    for (int g = 0; g < groups; ++g) {
+      const int t0 = g * tpb, t1 = std::min(t0 + tpb, ntiles);
+      const int jlo = (t0 / ftl) * 32, jhi0 = ((t1 - 1) / ftl + 1) * 32, jhi = std::min(jhi0, FinK);
+      span = std::max(span, jhi0 - jlo);
+      if (jhi - jlo > kDwNA * 64 * vw) ok = false;
+    }
+    if (ok) break;
+    if (tpb == 1) return hipErrorInvalidValue;
+  }
+  const size_t lds = size_t(kDwRB) * ((span | 1) + (((Fout + 31) & ~31) | 1)) * 4;
+  const dim3 grid(chunks, groups);
+  if (vw == 4)
+    hipLaunchKernelGGL(k_dw_slabs<4>, grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
+                       slab, pl_fin, pl_stride, K, tpb);
+  else
+    hipLaunchKernelGGL(k_dw_slabs<1>, grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
+                       slab, pl_fin, pl_stride, K, tpb);
   return hipGetLastError();
 }
 

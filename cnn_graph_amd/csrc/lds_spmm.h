@@ -1,0 +1,84 @@
+// One lane's piece of a CSR row product out of an LDS-resident operand, for
+// the resident kernels that keep both the sparse matrix (16-bit columns +
+// values) and the dense operand X ([rows][stride] floats) in LDS:
+//
+//   out[c0 .. c0+3] = sum_{j in row, CSR order} val[j] * X[col[j]][c0 .. c0+3]
+//
+// accumulated from +0 with one rounding per product and per add (the caller
+// compiles with fp contraction off) -- the order of lib/graph.py::chebyshev's
+// scipy csr_matvecs, so the result is bit-exact to it.  With a wave-uniform
+// bound L on the row length the entry loads and the gathers are unrolled and
+// issued together (the dynamic loop serialises one LDS round trip per entry);
+// entries past the row end read the zero row `zrow` with value 0, which adds
+// +0 to the sum.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace cg {
+
+template <int L>
+__device__ __forceinline__ float4 lds_row_spmm(const float* X, int stride, int c0,
+                                               const unsigned short* col, const float* val,
+                                               int rb, int re, int zrow) {
+#pragma clang fp contract(off)
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (L == 0) {  // any length
+    for (int jj = rb; jj < re; ++jj) {
+      const float w = val[jj];
+      const float4 g = *reinterpret_cast<const float4*>(X + int(col[jj]) * stride + c0);
+      s.x = s.x + w * g.x;
+      s.y = s.y + w * g.y;
+      s.z = s.z + w * g.z;
+      s.w = s.w + w * g.w;
+    }
+    return s;
+  }
+  int c[L > 0 ? L : 1];
+  float w[L > 0 ? L : 1];
+#pragma unroll
+  for (int e = 0; e < L; ++e) {
+    const bool ok = rb + e < re;
+    const int jj = ok ? rb + e : 0;
+    c[e] = ok ? int(col[jj]) : zrow;
+    w[e] = ok ? val[jj] : 0.f;
+  }
+  float4 g[L > 0 ? L : 1];
+#pragma unroll
+  for (int e = 0; e < L; ++e) g[e] = *reinterpret_cast<const float4*>(X + c[e] * stride + c0);
+#pragma unroll
+  for (int e = 0; e < L; ++e) {
+    s.x = s.x + w[e] * g[e].x;
+    s.y = s.y + w[e] * g[e].y;
+    s.z = s.z + w[e] * g[e].z;
+    s.w = s.w + w[e] * g[e].w;
+  }
+  return s;
+}
+
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
+
+// f(IntC<L>{}) with L the smallest supported unrolled bound >= len (0 = the
+// dynamic loop beyond 12); len must be wave-uniform
+template <typename F>
+__device__ __forceinline__ void with_row_len(int len, F&& f) {
+  if (len <= 4) f(IntC<4>{});
+  else if (len <= 6) f(IntC<6>{});
+  else if (len <= 8) f(IntC<8>{});
+  else if (len <= 10) f(IntC<10>{});
+  else if (len <= 12) f(IntC<12>{});
+  else f(IntC<0>{});
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int u = __shfl_xor(v, o);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+}  // namespace cg

@@ -16,7 +16,8 @@
 //   XCD under round-robin placement, so a pair's hand-off stays in one L2
 //   (speed only -- the hand-off protocol is agent-scope and placement-free).
 //   Each workgroup runs the whole Chebyshev recurrence of h (one 8-channel
-//   quarter at a time, two [M][8] LDS slots, CSR of L~ staged once in LDS)
+//   quarter at a time, two [M][8] LDS slots, CSR of L~ staged once in LDS,
+//   each wave's gathers unrolled to its longest row: lds_spmm.h)
 //   and the gate contraction on v_mfma_f32_32x32x2_f32 TRANSPOSED
 //   (gates x rows = Wh^T T^T): the B operand is the lane's own T_k values
 //   straight from the SpMM (no LDS read), and the accumulator leaves each
@@ -42,11 +43,12 @@
 //   computes dpre for 8 units x 4 gates of one row and feeds it as the B
 //   operand), then the reverse (Clenshaw) recurrence over the explicit L~^T
 //   G_{K-1} = D_{K-1}, G_k = (D_k + c L~^T G_{k+1}) - G_{k+2} (c = 2, 1 at
-//   k = 0) in two [M][16] LDS slots; workgroup u owns h channels
+//   k = 0) with G in one [M][16] LDS slot and L~^T staged in LDS; workgroup u owns h channels
 //   [16u, 16u + 16) of dh_prev = G_0 and stores the dpre / dc_prev of its
 //   units.  The h-weight gradient is summed afterwards per Chebyshev order
 //   over all steps from the forward's planes (one GEMM per order).
 #include "cg_internal.h"
+#include "lds_spmm.h"
 
 namespace cg {
 namespace {
@@ -77,6 +79,7 @@ struct SeqArgs {
   const int* rowptr;  // L~ (CSR, sorted columns)
   const int* col;
   const float* val;
+  const int* order;   // rows by decreasing length (lane -> row)
   int M, Mr, K, N, T, gates, nnz, P, pair_xcd;
   const float* gx;    // [T][N][M][128] x-conv gate pre-activations
   const float* Wh;    // [K*32][128], row c*K + k
@@ -131,14 +134,19 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
     s_col[e] = static_cast<unsigned short>(A.col[e]);
   }
   if (tid == 0) s_abort = 0;
-  int row[kRT], rb[kRT], re[kRT];
+  if (tid < 2 * kQ) (tid < kQ ? slot0 : slot1)[M * kQ + (tid & (kQ - 1))] = 0.f;  // zero row M
+  // lane (tile rt, j) owns row order[(wave + 8 rt) * 32 + j]: rows dealt by
+  // decreasing length, so a tile's rows have nearly equal lengths
+  int row[kRT], rb[kRT], re[kRT], wl[kRT];
   bool rv[kRT];
 #pragma unroll
   for (int rt = 0; rt < kRT; ++rt) {
-    row[rt] = (wave + 8 * rt) * 32 + j;
-    rv[rt] = row[rt] < M;
+    const int idx = (wave + 8 * rt) * 32 + j;
+    rv[rt] = idx < M;
+    row[rt] = rv[rt] ? A.order[idx] : M;
     rb[rt] = rv[rt] ? A.rowptr[row[rt]] : 0;
     re[rt] = rv[rt] ? A.rowptr[row[rt] + 1] : 0;
+    wl[rt] = wave_max(re[rt] - rb[rt]);  // the tile's longest row: its unrolled gather count
   }
   __syncthreads();
 
@@ -177,57 +185,50 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
             __syncthreads();
             if (s_abort) return;  // every thread of the workgroup returns here
           }
-          // T_0 quarter: registers + slot 0
-          float Tc[kRT][4];
+          // T_0 quarter into slot 0
 #pragma unroll
           for (int rt = 0; rt < kRT; ++rt) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s) Tc[rt][s] = 0.f;
             if (rv[rt]) {
               const float* p = hsrc + int64_t(row[rt]) * kH + 8 * q + 4 * hh;
-              if (t > 0) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) Tc[rt][s] = ld_sc1(p + s);
-              } else {
-                const float4 v = *reinterpret_cast<const float4*>(p);
-                Tc[rt][0] = v.x;
-                Tc[rt][1] = v.y;
-                Tc[rt][2] = v.z;
-                Tc[rt][3] = v.w;
-              }
-              *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) =
-                  make_float4(Tc[rt][0], Tc[rt][1], Tc[rt][2], Tc[rt][3]);
+              float4 v;
+              if (t > 0)
+                v = make_float4(ld_sc1(p), ld_sc1(p + 1), ld_sc1(p + 2), ld_sc1(p + 3));
+              else
+                v = *reinterpret_cast<const float4*>(p);
+              *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = v;
             }
           }
           __syncthreads();
           for (int k = 0; k < K; ++k) {
-            // gates^T += Wh_k^T T_k^T over this quarter's 8 channels
+            const float* cur = (k & 1) ? slot1 : slot0;
+            // gates^T += Wh_k^T T_k^T over this quarter's 8 channels; B operand:
+            // the lane's own T_k (its row in the slot; row M = zeros for idle lanes)
             const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
+            float4 tk[kRT];
+#pragma unroll
+            for (int rt = 0; rt < kRT; ++rt)
+              tk[rt] = *reinterpret_cast<const float4*>(cur + row[rt] * kQ + 4 * hh);
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
               const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
 #pragma unroll
               for (int rt = 0; rt < kRT; ++rt) {
-                acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, Tc[rt][s], acc[rt][0], 0, 0, 0);
-                acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, Tc[rt][s], acc[rt][1], 0, 0, 0);
+                const float b = (&tk[rt].x)[s];
+                acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[rt][0], 0, 0, 0);
+                acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[rt][1], 0, 0, 0);
               }
             }
             if (k + 1 < K) {
               // T_{k+1} of this lane's rows / channels: CSR order from +0
-              const float* cur = (k & 1) ? slot1 : slot0;
               float* nxt = (k & 1) ? slot0 : slot1;
 #pragma unroll
               for (int rt = 0; rt < kRT; ++rt) {
                 if (!rv[rt]) continue;
-                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-                for (int jj = rb[rt]; jj < re[rt]; ++jj) {
-                  const float w = s_val[jj];
-                  const float4 g = *reinterpret_cast<const float4*>(cur + int(s_col[jj]) * kQ + 4 * hh);
-                  s0 = s0 + w * g.x;
-                  s1 = s1 + w * g.y;
-                  s2 = s2 + w * g.z;
-                  s3 = s3 + w * g.w;
-                }
+                float4 sm;
+                with_row_len(wl[rt], [&](auto lc) {
+                  sm = lds_row_spmm<decltype(lc)::value>(cur, kQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+                });
+                float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
                 float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kQ + 4 * hh);
                 if (k >= 1) {  // T_{k-1} of this row: the slot being overwritten
                   const float4 p = *own;
@@ -242,10 +243,6 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
                   *reinterpret_cast<float4*>(A.planes + int64_t(k) * A.pstride +
                                              ((int64_t(t) * N + n) * M + row[rt]) * kH + 8 * q +
                                              4 * hh) = o;
-                Tc[rt][0] = s0;
-                Tc[rt][1] = s1;
-                Tc[rt][2] = s2;
-                Tc[rt][3] = s3;
               }
               __syncthreads();
             }
@@ -322,7 +319,8 @@ struct BStepArgs {
   const int* trowptr;  // L~^T (exact transpose, CSR)
   const int* tcol;
   const float* tval;
-  int M, Mr, N, gates, pair_xcd;
+  const int* order;    // rows of L~^T by decreasing length (lane -> row)
+  int M, Mr, N, gates, pair_xcd, nnz;
   const float* dh;      // [N][M][32] gradient of h' from above, or NULL
   const float* dh_rec;  // [N][M][32] gradient of h' from step t+1's h-conv, or NULL
   const float* dc;      // [N][M][32] gradient of c', or NULL
@@ -351,15 +349,31 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     n = blockIdx.x >> 1;
     u = blockIdx.x & 1;
   }
-  float* slotA = smem;
-  float* slotB = smem + A.Mr * kBS;
-  float* s_W = slotB + A.Mr * kBS;  // [K][s 32][q 4][i 16]
+  float* slot = smem;                // [Mr][16] G_{k+1} (row M: zeros)
+  float* s_W = slot + A.Mr * kBS;   // [K][s 32][q 4][i 16]
+  float* s_val = s_W + K * 2048;
+  unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
   // A operand of MFMA step s, order o: lane (i, q) holds Wh[(16u + i) K + o][g]
   // with g the gate column (s % 4) * 32 + 8q + s / 4 -- the column whose dpre
   // lane (row, q) supplies as the B operand at that step
   for (int e = tid; e < K * 2048; e += kST) {
     const int i = e & 15, qq = (e >> 4) & 3, s = (e >> 6) & 31, o = e >> 11;
     s_W[e] = A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
+  }
+  for (int e = tid; e < A.nnz; e += kST) {
+    s_val[e] = A.tval[e];
+    s_col[e] = static_cast<unsigned short>(A.tcol[e]);
+  }
+  if (tid < kBS) slot[M * kBS + tid] = 0.f;
+  // lane (tile rt, jr) owns row order[wave * 128 + 16 rt + jr]
+  int rows[kRB], rb[kRB], re[kRB], wl[kRB];
+#pragma unroll
+  for (int rt = 0; rt < kRB; ++rt) {
+    const int idx = wave * 128 + rt * 16 + jr;
+    rows[rt] = idx < M ? A.order[idx] : M;
+    rb[rt] = idx < M ? A.trowptr[rows[rt]] : 0;
+    re[rt] = idx < M ? A.trowptr[rows[rt] + 1] : 0;
+    wl[rt] = wave_max(re[rt] - rb[rt]);
   }
   __syncthreads();
   f32x4 acc[kRB][K];
@@ -369,10 +383,10 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     for (int o = 0; o < K; ++o) acc[rt][o] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool ref = A.gates == 0;
   const bool own = (q >> 1) == u;  // this lane's units are stored by this workgroup
-  // phase A: dpre of units 8q .. 8q+7 of rows wave*128 + 16 rt + jr, and D_o
+  // phase A: dpre of units 8q .. 8q+7 of the lane's rows, and D_o
 #pragma unroll
   for (int rt = 0; rt < kRB; ++rt) {
-    const int row = wave * 128 + rt * 16 + jr;
+    const int row = rows[rt];
     float dp[4][8];
     if (row < M) {
       const int64_t rr = int64_t(n) * M + row;
@@ -450,7 +464,9 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
                                                           0, 0, 0);
     }
   }
-  // phase B: lane (row, q) holds D_o[row][16u + 4q + r] in acc[rt][o][r]
+  // phase B: lane (row, q) holds D_o[row][16u + 4q + r] in acc[rt][o][r];
+  // G_{k+1} of all rows in the LDS slot, G_{k+2} / G_{k+1} of the lane's own
+  // rows in registers; one slot: gather, barrier, overwrite, barrier
   float G1[kRB][4], G2[kRB][4];
 #pragma unroll
   for (int rt = 0; rt < kRB; ++rt)
@@ -459,67 +475,53 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
       G1[rt][r] = acc[rt][K - 1][r];
       G2[rt][r] = 0.f;
     }
-  if (K > 1) {
+  auto put = [&]() {
 #pragma unroll
-    for (int rt = 0; rt < kRB; ++rt) {
-      const int row = wave * 128 + rt * 16 + jr;
-      if (row < M)
-        *reinterpret_cast<float4*>(slotA + row * kBS + 4 * q) =
+    for (int rt = 0; rt < kRB; ++rt)
+      if (rows[rt] < M)
+        *reinterpret_cast<float4*>(slot + rows[rt] * kBS + 4 * q) =
             make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
-    }
+  };
+  if (K > 1) {
+    put();
     __syncthreads();
   }
 #pragma unroll
   for (int k = K - 2; k >= 0; --k) {
-    const float* cur = ((K - 2 - k) & 1) ? slotB : slotA;
-    float* nxt = ((K - 2 - k) & 1) ? slotA : slotB;
     const float cc = k >= 1 ? 2.f : 1.f;
+    float Gn[kRB][4];
 #pragma unroll
     for (int rt = 0; rt < kRB; ++rt) {
-      const int row = wave * 128 + rt * 16 + jr;
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      if (row < M) {
-        const int j0 = A.trowptr[row], j1 = A.trowptr[row + 1];
-        for (int jb = j0; jb < j1; jb += 8) {
-          int cidx[8];
-          float ww[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int jj = (jb + e < j1) ? jb + e : j1 - 1;
-            cidx[e] = A.tcol[jj];
-            ww[e] = A.tval[jj];
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float4 g = *reinterpret_cast<const float4*>(cur + cidx[e] * kBS + 4 * q);
-            if (jb + e < j1) {
-              s0 = s0 + ww[e] * g.x;
-              s1 = s1 + ww[e] * g.y;
-              s2 = s2 + ww[e] * g.z;
-              s3 = s3 + ww[e] * g.w;
-            }
-          }
-        }
-      }
-      const float sv[4] = {s0, s1, s2, s3};
+      float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rows[rt] < M)
+        with_row_len(wl[rt], [&](auto lc) {
+          sm = lds_row_spmm<decltype(lc)::value>(slot, kBS, 4 * q, s_col, s_val, rb[rt], re[rt], M);
+        });
+      const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float gk = acc[rt][k][r] + cc * sv[r];
         if (k + 2 <= K - 1) gk = gk - G2[rt][r];
-        G2[rt][r] = G1[rt][r];
-        G1[rt][r] = gk;
+        Gn[rt][r] = gk;
       }
-      if (k > 0 && row < M)
-        *reinterpret_cast<float4*>(nxt + row * kBS + 4 * q) =
-            make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
     }
-    if (k > 0) __syncthreads();
+#pragma unroll
+    for (int rt = 0; rt < kRB; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        G2[rt][r] = G1[rt][r];
+        G1[rt][r] = Gn[rt][r];
+      }
+    if (k > 0) {
+      __syncthreads();  // every gather of G_{k+1} done
+      put();
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int rt = 0; rt < kRB; ++rt) {
-    const int row = wave * 128 + rt * 16 + jr;
-    if (row < M)
-      *reinterpret_cast<float4*>(A.dh_prev + (int64_t(n) * M + row) * kH + 16 * u + 4 * q) =
+    if (rows[rt] < M)
+      *reinterpret_cast<float4*>(A.dh_prev + (int64_t(n) * M + rows[rt]) * kH + 16 * u + 4 * q) =
           make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
   }
 }
@@ -529,7 +531,7 @@ inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
 }  // namespace
 
 size_t lstm_seq_lds(int M, int K, int64_t nnz) {
-  return size_t(2) * round_up(M, 32) * kQ * 4 + size_t(K) * 2048 * 4 + 512 + size_t(nnz) * 4 +
+  return size_t(2) * round_up(M + 1, 32) * kQ * 4 + size_t(K) * 2048 * 4 + 512 + size_t(nnz) * 4 +
          align16(size_t(nnz) * 2);
 }
 
@@ -538,13 +540,14 @@ bool lstm_seq_ok(int M, int H, int K, int64_t nnz) {
          lstm_seq_lds(M, K, nnz) <= size_t(kLdsBytes - kSeqStaticLds);
 }
 
-size_t lstm_bstep_lds(int M, int K) {
-  return size_t(2) * round_up(M, 16) * kBS * 4 + size_t(K) * 2048 * 4;
+size_t lstm_bstep_lds(int M, int K, int64_t nnzT) {
+  return size_t(round_up(M + 1, 16)) * kBS * 4 + size_t(K) * 2048 * 4 + size_t(nnzT) * 4 +
+         align16(size_t(nnzT) * 2);
 }
 
-bool lstm_bstep_ok(int M, int H, int K) {
-  return H == kH && M >= 1 && M <= kRB * 8 * 16 && K >= 1 && K <= 4 &&
-         lstm_bstep_lds(M, K) <= size_t(kLdsBytes);
+bool lstm_bstep_ok(int M, int H, int K, int64_t nnzT) {
+  return H == kH && M >= 1 && M <= kRB * 8 * 16 && K >= 1 && K <= 4 && nnzT >= 1 &&
+         lstm_bstep_lds(M, K, nnzT) <= size_t(kLdsBytes);
 }
 
 int lstm_seq_pairs(int N, int device) {
@@ -557,7 +560,7 @@ int lstm_seq_pairs(int N, int device) {
 }
 
 hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, const int* rowptr,
-                           const int* col, const float* val, const float* gx, const float* Wh,
+                           const int* col, const float* val, const int* order, const float* gx, const float* Wh,
                            const float* bias, const float* h0, const float* c0, float* hs,
                            float* cs, float* act, float* planes, int64_t pstride, int* flags,
                            int* status, int P, hipStream_t s) {
@@ -573,7 +576,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
       rate_khz <= 0)
     rate_khz = 100000;  // 100 MHz
-  SeqArgs a{rowptr, col, val, M, round_up(M, 32), K, N, T, gates, int(nnz), P,
+  SeqArgs a{rowptr, col, val, order, M, round_up(M + 1, 32), K, N, T, gates, int(nnz), P,
             P % 8 == 0 ? 1 : 0, gx, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
             // a pair hand-off that has not happened after 2 s ends the launch
             static_cast<unsigned long long>(rate_khz) * 2000ull};
@@ -596,14 +599,14 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
 }
 
 hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr, const int* tcol,
-                             const float* tval, const float* dh, const float* dh_rec,
+                             const float* tval, const int* order, int64_t nnzT, const float* dh, const float* dh_rec,
                              const float* dc, const float* act, const float* c_prev,
                              const float* c_out, const float* Wh, float* dpre, float* dc_prev,
                              float* dh_prev, hipStream_t s) {
-  if (!lstm_bstep_ok(M, kH, K) || N < 1) return hipErrorInvalidValue;
-  BStepArgs a{trowptr, tcol, tval, M, round_up(M, 16), N, gates, N % 8 == 0 ? 1 : 0, dh, dh_rec,
-              dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev};
-  const size_t lds = lstm_bstep_lds(M, K);
+  if (!lstm_bstep_ok(M, kH, K, nnzT) || N < 1) return hipErrorInvalidValue;
+  BStepArgs a{trowptr, tcol, tval, order, M, round_up(M + 1, 16), N, gates, N % 8 == 0 ? 1 : 0,
+              int(nnzT), dh, dh_rec, dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev};
+  const size_t lds = lstm_bstep_lds(M, K, nnzT);
 #define CG_BSTEP(KK)                                                                              \
   case KK: {                                                                                      \
     static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_bstep<KK>), \

@@ -58,8 +58,11 @@ enum {
   CG_VARIANT_AUTO = 0,       /* fastest kernels that fit (cheb_fast when it applies)  */
   CG_VARIANT_CLASSIC = 1,    /* classic resident kernels (cheb_resident)              */
   CG_VARIANT_UNFUSED_DW = 2, /* fast kernels, dW by the separate streaming GEMM       */
-  CG_VARIANT_NARROW = 3      /* streaming path in the sample-major layout even where
+  CG_VARIANT_NARROW = 3,     /* streaming path in the sample-major layout even where
                                 the wide-column layout (Fin < 8) would apply          */
+  CG_VARIANT_STEPS = 4       /* streaming path with one launch per Chebyshev step even
+                                where the channel-group resident kernels apply
+                                (M <= 1024, Fin % 8 == 0)                             */
 };
 
 typedef struct cg_plan cg_plan;

@@ -117,6 +117,46 @@ def test_resgnn_train_steps_vs_oracle(dev, graph, R, Fin, F):
             assert O.normwise_err(f64(w), rw) < TOL, (step, name)
 
 
+def test_resgnn_humanflow_shape_train_steps_vs_oracle(dev):
+    """Config R's shape (the humanflow-ln-period ResGNN, SURVEY.md §6: K = 20,
+    nfilter = 32, nres_layer_count = 4, Fin = 2, on config E's 1024-vertex
+    graph) at a small batch: three optimizer steps vs the float64 oracle --
+    loss, every dW and every updated W -- with the hidden layers' saved basis
+    in the planes layout (the layout the config-R bench runs)."""
+    from cnn_graph_amd.model import ResGNN
+    L, _ = golden_L("golden_E.npz")
+    N, K, F, R, Fin = 3, 20, 32, 4, 2
+    model = ResGNN(L, N=N, Fin=Fin, nfilter=F, K=K, nres_layer_count=R, learning_rate=1e-3,
+                   decay_rate=0.95, decay_steps=2, device=dev, seed=13)
+    from cnn_graph_amd import ops
+    assert ops.basis_layout_for(model.plan, N, F, K, F) == "planes"
+    assert model.net.layout.count("planes") >= 2 * R  # the 8 hidden 32 -> 32 filters
+    lap = (model.plan.rowptr, model.plan.col, model.plan.val.astype(np.float64))
+    rng = np.random.default_rng(17)
+    x = rng.random((N, model.M, Fin)).astype(np.float32)
+    labels = rng.random((N, model.M, 2)).astype(np.float32)
+    # Adam's early steps move each weight by ~lr * sign(g) whatever |g|, so the
+    # updated weights are ill-conditioned in the gradients' rounding at K = 20:
+    # the oracle recomputes loss and gradients from the GPU's weights of each
+    # step, and the update is checked as the oracle's Adam of the GPU gradient
+    state = [(np.zeros_like(f64(w)), np.zeros_like(f64(w))) for w in model.W]
+    for step in range(1, 4):
+        Wprev = [f64(w) for w in model.W]
+        loss = model.train_step(t(x, dev), t(labels, dev))
+        torch.cuda.synchronize()
+        lr = model.learning_rate(step - 1)
+        rl, rdW, _, _ = MO.train_step(x.astype(np.float64), labels, Wprev, lap, K, R, state, step, lr)
+        assert abs(float(loss.item()) - rl) <= 1e-5 * rl, (step, float(loss.item()), rl)
+        for name, g, rg in zip(model.names, model.dW, rdW):
+            assert O.normwise_err(f64(g), rg) < TOL, (step, name)
+        new_state = []
+        for name, w, w0, g, (m, v) in zip(model.names, model.W, Wprev, model.dW, state):
+            rw, m2, v2 = O.adam_step(w0, f64(g), m, v, step, lr=lr)
+            new_state.append((m2, v2))
+            assert O.normwise_err(f64(w), rw) < TOL, (step, name)
+        state = new_state
+
+
 def test_graphconv_residual_network_autograd_matches_trainer(dev):
     """GraphConv.residual_network (torch autograd over the fused epilogue ops)
     gives the same gradients as the explicit ResGNN schedule."""
