@@ -81,6 +81,8 @@ _SIGNATURES = {
     "cg_stack_merge_backward": ([_c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp], _c_int),
     "cg_weight_grad_workspace_bytes": ([_c_i64, _c_i32, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
     "cg_weight_grad": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
+    "cg_weight_grad_planes": ([_c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _c_i32, _vp, _c_sz,
+                               _vp], _c_int),
     "cg_bias_grad_workspace_bytes": ([_c_i64, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
     "cg_bias_grad": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
     "cg_bias_act_forward": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp], _c_int),

@@ -1211,6 +1211,23 @@ int cg_weight_grad(int64_t R, int32_t FinK, int32_t Fout, const float* basis, co
   return ok();
 }
 
+int cg_weight_grad_planes(int64_t R, int32_t Fin, int32_t K, int32_t Fout, const float* planes,
+                          int64_t plane_stride, const float* dy, float* dW, int32_t accumulate,
+                          void* workspace, size_t ws_bytes, void* stream) {
+  if (!planes || !dy || !dW || R < 1 || Fin < 1 || K < 1 || Fout < 1 || plane_stride < R * Fin)
+    return fail(CG_ERR_ARG, "weight_grad_planes: bad arguments");
+  const int FinK = Fin * K;
+  const size_t need = dw_slab_bytes(R, 0, FinK, Fout);
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "weight_grad_planes workspace too small: %zu < %zu", ws_bytes, need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float* slabs = static_cast<float*>(workspace);
+  CG_HIP(cg::launch_dw_slabs(planes, dy, R, FinK, Fout, slabs, s, Fin, plane_stride, K));
+  CG_HIP(cg::launch_reduce_slabs_acc(slabs, cg::dw_chunks(R), int64_t(FinK) * Fout, dW,
+                                     accumulate != 0, s));
+  return ok();
+}
+
 int cg_bias_grad_workspace_bytes(int64_t R, int32_t C, size_t* bytes) {
   if (!bytes || R < 1 || C < 1) return fail(CG_ERR_ARG, "bias_grad: bad arguments");
   *bytes = al256(size_t(cg::colsum_chunks(R)) * size_t(C) * 4);
@@ -1467,6 +1484,9 @@ int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t 
                                     "weights in LDS (M=%d nnz=%lld H=%d K=%d)",
                 plan->M, (long long)plan->nnz, H, K);
   const int64_t R = int64_t(T) * N * plan->M;
+  if (!planes && K > 1)
+    return fail(CG_ERR_ARG, "lstm_seq_forward: planes are required for K > 1 (the pair hands "
+                            "its quarters' Chebyshev orders to the partner through them)");
   if (planes && K > 1 && plane_stride < R * H)
     return fail(CG_ERR_ARG, "lstm_seq_forward: plane stride %lld < T*N*M*H", (long long)plane_stride);
   if (!al16(gx) || !al16(hs) || !al16(cs) || (act && !al16(act)) || (planes && !al16(planes)) ||

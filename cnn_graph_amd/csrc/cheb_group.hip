@@ -93,29 +93,30 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
     s_col[e] = static_cast<unsigned short>(A.col[e]);
   }
   if (tid < 2 * kGQ) (tid < kGQ ? slot0 : slot1)[M * kGQ + (tid & (kGQ - 1))] = 0.f;  // zero row M
-  int row[kGRT], rb[kGRT], re[kGRT], wl[kGRT];
-  bool rv[kGRT];
-  float Tc[kGRT][4];
-  const int c0 = kGQ * g + 4 * hh;
+  // two lane mappings over the same 32 rows of tile (wave, rt): the MFMA's
+  // (row j = lane % 32, half hh = lane / 32) reads its B operand from the slot;
+  // the SpMM's (row lane / 2, half lane % 2) makes an 8-lane LDS access group
+  // gather 4 whole 32-byte records
+  const int js = lane >> 1, hs = lane & 1;
+  int row[kGRT], rowS[kGRT], rb[kGRT], re[kGRT], wl[kGRT];
+  bool rvS[kGRT];
+  const int c0 = kGQ * g + 4 * hs;
 #pragma unroll
   for (int rt = 0; rt < kGRT; ++rt) {
     const int idx = (wave + 8 * rt) * 32 + j;
-    rv[rt] = idx < M;
-    row[rt] = rv[rt] ? A.order[idx] : M;
-    rb[rt] = rv[rt] ? A.rowptr[row[rt]] : 0;
-    re[rt] = rv[rt] ? A.rowptr[row[rt] + 1] : 0;
+    row[rt] = idx < M ? A.order[idx] : M;
+    const int idxS = (wave + 8 * rt) * 32 + js;
+    rvS[rt] = idxS < M;
+    rowS[rt] = rvS[rt] ? A.order[idxS] : M;
+    rb[rt] = rvS[rt] ? A.rowptr[rowS[rt]] : 0;
+    re[rt] = rvS[rt] ? A.rowptr[rowS[rt] + 1] : 0;
     wl[rt] = wave_max(re[rt] - rb[rt]);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rv[rt]) {
-      const int64_t o = (int64_t(n) * M + row[rt]) * Fin + c0;
-      v = *reinterpret_cast<const float4*>(A.x + o);
+    if (rvS[rt]) {
+      const int64_t o = (int64_t(n) * M + rowS[rt]) * Fin + c0;
+      const float4 v = *reinterpret_cast<const float4*>(A.x + o);
       *reinterpret_cast<float4*>(A.basis + o) = v;  // plane 0 = x
-      *reinterpret_cast<float4*>(slot0 + row[rt] * kGQ + 4 * hh) = v;
+      *reinterpret_cast<float4*>(slot0 + rowS[rt] * kGQ + 4 * hs) = v;
     }
-    Tc[rt][0] = v.x;
-    Tc[rt][1] = v.y;
-    Tc[rt][2] = v.z;
-    Tc[rt][3] = v.w;
   }
   f32x16 acc[kGRT][NOT];
 #pragma unroll
@@ -126,9 +127,14 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
       for (int e = 0; e < 16; ++e) acc[rt][ot][e] = 0.f;
   __syncthreads();
   for (int k = 0; k < K; ++k) {
+    const float* cur = (k & 1) ? slot1 : slot0;
     if (want_y) {
       // y^T[out][row] += W_k^T[out][ch] T_k^T[ch][row], channels 4hh + s
       const float* wk = s_W + k * 256 * NOT + hh * 32 * NOT + j;
+      float4 tk[kGRT];
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt)
+        tk[rt] = *reinterpret_cast<const float4*>(cur + row[rt] * kGQ + 4 * hh);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -136,22 +142,21 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
           const float a = wk[s * 64 * NOT + ot * 32];
 #pragma unroll
           for (int rt = 0; rt < kGRT; ++rt)
-            acc[rt][ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Tc[rt][s], acc[rt][ot], 0, 0, 0);
+            acc[rt][ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, (&tk[rt].x)[s], acc[rt][ot], 0, 0, 0);
         }
     }
     if (k + 1 < K) {
-      const float* cur = (k & 1) ? slot1 : slot0;
       float* nxt = (k & 1) ? slot0 : slot1;
       float* pl = A.basis + int64_t(k + 1) * A.plane;
 #pragma unroll
       for (int rt = 0; rt < kGRT; ++rt) {
-        if (!rv[rt]) continue;
+        if (!rvS[rt]) continue;
         float4 sm;
         with_row_len(wl[rt], [&](auto lc) {
-          sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+          sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hs, s_col, s_val, rb[rt], re[rt], M);
         });
         float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
-        float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kGQ + 4 * hh);
+        float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kGQ + 4 * hs);
         if (k >= 1) {  // T_{k-1}: the slot entry being overwritten
           const float4 p = *own;
           s0 = 2.f * s0 - p.x;
@@ -161,11 +166,7 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
         }
         const float4 o = make_float4(s0, s1, s2, s3);
         *own = o;
-        *reinterpret_cast<float4*>(pl + (int64_t(n) * M + row[rt]) * Fin + c0) = o;
-        Tc[rt][0] = s0;
-        Tc[rt][1] = s1;
-        Tc[rt][2] = s2;
-        Tc[rt][3] = s3;
+        *reinterpret_cast<float4*>(pl + (int64_t(n) * M + rowS[rt]) * Fin + c0) = o;
       }
       __syncthreads();
     }
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
   float* yg = A.yp + int64_t(g) * A.N * M * Fout;
 #pragma unroll
   for (int rt = 0; rt < kGRT; ++rt) {
-    if (!rv[rt]) continue;
+    if (row[rt] >= M) continue;
     float* yr = yg + (int64_t(n) * M + row[rt]) * Fout;
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
@@ -225,7 +226,9 @@ __global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j = lane & 31, hh = lane >> 5;
+  // lanes 2j, 2j+1 take the two 16-byte halves of row j's 32-byte record, so
+  // an 8-lane LDS access group gathers 4 whole records (4 bank groups of 8)
+  const int j = lane >> 1, hh = lane & 1;
   int n, g;
   grp_map(blockIdx.x, A.G, n, g);
   if (n >= A.N) return;

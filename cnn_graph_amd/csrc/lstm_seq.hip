@@ -75,6 +75,22 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 16 bytes as two 8-byte agent-scope accesses (global_load/store_dwordx2 sc1)
+__device__ __forceinline__ float4 ld16_sc1(const float* p) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(const_cast<float*>(p));
+  const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float4(__uint_as_float(unsigned(a)), __uint_as_float(unsigned(a >> 32)),
+                     __uint_as_float(unsigned(b)), __uint_as_float(unsigned(b >> 32)));
+}
+__device__ __forceinline__ void st16_sc1(float* p, float4 v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  __hip_atomic_store(q, (unsigned long long)(__float_as_uint(v.x)) | ((unsigned long long)(__float_as_uint(v.y)) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, (unsigned long long)(__float_as_uint(v.z)) | ((unsigned long long)(__float_as_uint(v.w)) << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct SeqArgs {
   const int* rowptr;  // L~ (CSR, sorted columns)
   const int* col;
@@ -94,6 +110,9 @@ struct SeqArgs {
   int* flags;         // [P][2] step counters (zeroed before the launch)
   int* status;        // [1] 0 = ok, 1 = a hand-off timed out
   unsigned long long timeout;  // wall-clock ticks
+  int dbg;            // ablation build only (CG_DBG): 1 no MFMA, 2 no SpMM, 4 no gate math,
+                      // 8 no partner wait, 16 no gx / c loads, 32 no plane stores
+  unsigned long long* ts;  // ablation build: phase stamps of step 1 (CG_TS), else NULL
 };
 
 __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
@@ -137,15 +156,21 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
   if (tid < 2 * kQ) (tid < kQ ? slot0 : slot1)[M * kQ + (tid & (kQ - 1))] = 0.f;  // zero row M
   // lane (tile rt, j) owns row order[(wave + 8 rt) * 32 + j]: rows dealt by
   // decreasing length, so a tile's rows have nearly equal lengths
-  int row[kRT], rb[kRT], re[kRT], wl[kRT];
-  bool rv[kRT];
+  // the SpMM lanes take the same 32 rows of a tile as (row lane / 2, half
+  // lane % 2): an 8-lane LDS access group gathers 4 whole 32-byte records
+  const int js = lane >> 1, hs2 = lane & 1;
+  int row[kRT], rowS[kRT], rb[kRT], re[kRT], wl[kRT];
+  bool rv[kRT], rvS[kRT];
 #pragma unroll
   for (int rt = 0; rt < kRT; ++rt) {
     const int idx = (wave + 8 * rt) * 32 + j;
     rv[rt] = idx < M;
     row[rt] = rv[rt] ? A.order[idx] : M;
-    rb[rt] = rv[rt] ? A.rowptr[row[rt]] : 0;
-    re[rt] = rv[rt] ? A.rowptr[row[rt] + 1] : 0;
+    const int idxS = (wave + 8 * rt) * 32 + js;
+    rvS[rt] = idxS < M;
+    rowS[rt] = rvS[rt] ? A.order[idxS] : M;
+    rb[rt] = rvS[rt] ? A.rowptr[rowS[rt]] : 0;
+    re[rt] = rvS[rt] ? A.rowptr[rowS[rt] + 1] : 0;
     wl[rt] = wave_max(re[rt] - rb[rt]);  // the tile's longest row: its unrolled gather count
   }
   __syncthreads();
@@ -155,6 +180,8 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
   for (int n = pair, it = 0; n < N; n += A.P, ++it) {
     const int base = it * T;
     for (int t = 0; t < T; ++t) {
+      const bool stamp = (t == 1 && it == 0);
+      if (stamp) CG_TS(A.ts, 0);
       f32x16 acc[kRT][2];
 #pragma unroll
       for (int rt = 0; rt < kRT; ++rt)
@@ -162,74 +189,58 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
         for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[rt][ct][e] = 0.f;
-      if (t > 0 || A.h0) {
-        const float* hsrc = (t == 0) ? A.h0 + int64_t(n) * M * kH
-                                     : A.hs + (int64_t(t - 1) * N + n) * M * kH;
-        for (int qi = 0; qi < 4; ++qi) {
-          const int q = (2 * u + qi) & 3;  // own quarters first
-          if (qi == 2 && t > 0) {
-            // the partner's half of h_{t-1}: wait for its step t-1 counter
-            if (tid == 0) {
-              const int need = base + t;
-              const unsigned long long t0 = wall_clock64();
-              while (__hip_atomic_load(const_cast<int*>(partner_flag), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT) < need) {
-                __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > A.timeout) {
-                  s_abort = 1;
-                  __hip_atomic_store(A.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  break;
-                }
-              }
-            }
-            __syncthreads();
-            if (s_abort) return;  // every thread of the workgroup returns here
+      const bool has_h = t > 0 || A.h0;
+      const float* hsrc = (t == 0) ? A.h0 + int64_t(n) * M * kH
+                                   : A.hs + (int64_t(t - 1) * N + n) * M * kH;
+      float* pl_t = A.planes + (int64_t(t) * N + n) * M * kH;  // plane k at + (k-1)*pstride
+      // gates^T += Wh_k^T T_k^T over quarter q's 8 channels; B operand: the
+      // lane's own rows of T_k (tk, channels 8q + 4hh .. +3)
+      auto contract = [&](int q, int k, const float4* tk) {
+        const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
+#pragma unroll
+        for (int s = 0; s < 4 && !CG_DBG(A.dbg, 1); ++s) {
+          const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
+#pragma unroll
+          for (int rt = 0; rt < kRT; ++rt) {
+            const float b = (&tk[rt].x)[s];
+            acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[rt][0], 0, 0, 0);
+            acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[rt][1], 0, 0, 0);
           }
-          // T_0 quarter into slot 0
+        }
+      };
+      if (has_h) {
+        // the two OWN quarters (units 16u .. 16u+15): the recurrence in LDS,
+        // T_1 .. T_{K-1} leave as basis planes (write-through: the partner reads them)
+        for (int qq = 0; qq < 2; ++qq) {
+          const int q = 2 * u + qq;
 #pragma unroll
           for (int rt = 0; rt < kRT; ++rt) {
             if (rv[rt]) {
               const float* p = hsrc + int64_t(row[rt]) * kH + 8 * q + 4 * hh;
-              float4 v;
-              if (t > 0)
-                v = make_float4(ld_sc1(p), ld_sc1(p + 1), ld_sc1(p + 2), ld_sc1(p + 3));
-              else
-                v = *reinterpret_cast<const float4*>(p);
+              const float4 v = (t > 0) ? ld16_sc1(p) : *reinterpret_cast<const float4*>(p);
               *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = v;
             }
           }
           __syncthreads();
           for (int k = 0; k < K; ++k) {
             const float* cur = (k & 1) ? slot1 : slot0;
-            // gates^T += Wh_k^T T_k^T over this quarter's 8 channels; B operand:
-            // the lane's own T_k (its row in the slot; row M = zeros for idle lanes)
-            const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
             float4 tk[kRT];
 #pragma unroll
             for (int rt = 0; rt < kRT; ++rt)
               tk[rt] = *reinterpret_cast<const float4*>(cur + row[rt] * kQ + 4 * hh);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
-#pragma unroll
-              for (int rt = 0; rt < kRT; ++rt) {
-                const float b = (&tk[rt].x)[s];
-                acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[rt][0], 0, 0, 0);
-                acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[rt][1], 0, 0, 0);
-              }
-            }
+            contract(q, k, tk);
             if (k + 1 < K) {
               // T_{k+1} of this lane's rows / channels: CSR order from +0
               float* nxt = (k & 1) ? slot0 : slot1;
 #pragma unroll
               for (int rt = 0; rt < kRT; ++rt) {
-                if (!rv[rt]) continue;
+                if (!rvS[rt] || CG_DBG(A.dbg, 2)) continue;
                 float4 sm;
                 with_row_len(wl[rt], [&](auto lc) {
-                  sm = lds_row_spmm<decltype(lc)::value>(cur, kQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+                  sm = lds_row_spmm<decltype(lc)::value>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
                 });
                 float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
-                float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kQ + 4 * hh);
+                float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2);
                 if (k >= 1) {  // T_{k-1} of this row: the slot being overwritten
                   const float4 p = *own;
                   s0 = 2.f * s0 - p.x;
@@ -239,16 +250,60 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
                 }
                 const float4 o = make_float4(s0, s1, s2, s3);
                 *own = o;
-                if (A.planes && (q >> 1) == u)
-                  *reinterpret_cast<float4*>(A.planes + int64_t(k) * A.pstride +
-                                             ((int64_t(t) * N + n) * M + row[rt]) * kH + 8 * q +
-                                             4 * hh) = o;
+                if (!CG_DBG(A.dbg, 32))
+                  st16_sc1(pl_t + int64_t(k) * A.pstride + int64_t(rowS[rt]) * kH + 8 * q + 4 * hs2, o);
               }
               __syncthreads();
             }
           }
         }
       }
+      if (stamp) CG_TS(A.ts, 1);
+      // publish: h_{t-1} of this workgroup's units (stored by the previous
+      // step's epilogue, drained here -- its stores overlapped the own
+      // quarters above) and the own quarters' planes of step t
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(my_flag, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (has_h) {
+        if (!CG_DBG(A.dbg, 8)) {
+          // the partner's quarters of step t: wait for its counter
+          if (tid == 0) {
+            const int need = base + t + 1;
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(const_cast<int*>(partner_flag), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) < need) {
+              __builtin_amdgcn_s_sleep(1);
+              if (wall_clock64() - t0 > A.timeout) {
+                s_abort = 1;
+                __hip_atomic_store(A.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+            }
+          }
+          __syncthreads();
+          if (s_abort) return;  // every thread of the workgroup returns here
+        }
+        if (stamp) CG_TS(A.ts, 2);
+        // the partner's two quarters: T_0 = its half of h_{t-1}, T_k its planes
+        // (sc1 loads, no recurrence here: it computed them)
+        for (int qq = 0; qq < 2; ++qq) {
+          const int q = 2 * (1 - u) + qq;
+          for (int k = 0; k < K; ++k) {
+            const float* src = (k == 0) ? hsrc : pl_t + int64_t(k - 1) * A.pstride;
+            float4 tk[kRT];
+#pragma unroll
+            for (int rt = 0; rt < kRT; ++rt) {
+              const float* p = src + int64_t(row[rt]) * kH + 8 * q + 4 * hh;
+              tk[rt] = !rv[rt] ? make_float4(0.f, 0.f, 0.f, 0.f)
+                               : (k == 0 && t == 0) ? *reinterpret_cast<const float4*>(p)
+                                                    : ld16_sc1(p);
+            }
+            contract(q, k, tk);
+          }
+        }
+      }
+      if (stamp) CG_TS(A.ts, 3);
       // gate update: lane (row, hh) of tile (rt, ct) holds gates g = 0..3 of
       // units 16u + 8ct + 4hh + m in acc[rt][ct][4g + m]
 #pragma unroll
@@ -261,11 +316,13 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           float4 gv[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            gv[g] = *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
+            gv[g] = CG_DBG(A.dbg, 16) ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                      : *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
           // c_{t-1}: this lane's own store of the previous step (same address,
           // same lane), or the initial state
           float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (t > 0)
+          if (CG_DBG(A.dbg, 16)) {
+          } else if (t > 0)
             cv = *reinterpret_cast<const float4*>(A.cs + (rr - int64_t(N) * M) * kH + u0);
           else if (A.c0)
             cv = *reinterpret_cast<const float4*>(A.c0 + (int64_t(n) * M + row[rt]) * kH + u0);
@@ -283,12 +340,24 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
               af = af + s_b[64 + u0 + m];
               ao = ao + s_b[96 + u0 + m];
             }
-            const float z = A.gates == 0 ? tanf(az) : tanhf(az);
-            const float ig = sigm(ai), fg = sigm(af);
-            const float o = A.gates == 0 ? tanhf(ao) : sigm(ao);
-            const float cn = fg * c[m] + ig * z;
-            c[m] = cn;
-            hn[m] = o * tanhf(cn);
+            float z, ig, fg, o, cn;
+            if (CG_DBG(A.dbg, 4)) {
+              z = az;
+              ig = ai;
+              fg = af;
+              o = ao;
+              cn = c[m] + az;
+              c[m] = cn;
+              hn[m] = ao * cn;
+            } else {
+              z = A.gates == 0 ? tanf(az) : tanhf(az);
+              ig = sigm(ai);
+              fg = sigm(af);
+              o = A.gates == 0 ? tanhf(ao) : sigm(ao);
+              cn = fg * c[m] + ig * z;
+              c[m] = cn;
+              hn[m] = o * tanhf(cn);
+            }
             zz[m] = z;
             ii[m] = ig;
             ff[m] = fg;
@@ -296,8 +365,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           }
           *reinterpret_cast<float4*>(A.cs + rr * kH + u0) =
               make_float4(c[0], c[1], c[2], c[3]);
-#pragma unroll
-          for (int m = 0; m < 4; ++m) st_sc1(A.hs + rr * kH + u0 + m, hn[m]);
+          st16_sc1(A.hs + rr * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
           if (A.act) {
             float* ap = A.act + rr * 128 + u0;
             *reinterpret_cast<float4*>(ap) = make_float4(zz[0], zz[1], zz[2], zz[3]);
@@ -307,10 +375,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           }
         }
       }
-      // publish h_t: every wave drains its stores, then one flag store
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(my_flag, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stamp) CG_TS(A.ts, 4);
     }
   }
 }
@@ -579,7 +644,11 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   SeqArgs a{rowptr, col, val, order, M, round_up(M + 1, 32), K, N, T, gates, int(nnz), P,
             P % 8 == 0 ? 1 : 0, gx, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
             // a pair hand-off that has not happened after 2 s ends the launch
-            static_cast<unsigned long long>(rate_khz) * 2000ull};
+            static_cast<unsigned long long>(rate_khz) * 2000ull, (debug_flags() >> 16) & 0xff,
+            nullptr};
+#ifdef CG_DEBUG
+  a.ts = g_debug_ts;
+#endif
   hipError_t e = hipMemsetAsync(flags, 0, sizeof(int) * (size_t(2) * P + 1), s);
   if (e != hipSuccess) return e;
   // a pair waits for its partner, so every workgroup of the grid must be

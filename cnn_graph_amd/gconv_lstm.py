@@ -244,13 +244,23 @@ class _Layer(torch.autograd.Function):
         fused = cell.fused or cell.seq
         # h bases kept for the backward's weight gradient: the fused h-step
         # writes the orders 1..K-1 as planes [K-1][T][R][H] (order 0 is h_prev)
-        planes = torch.empty((max(K - 1, 1), T, R, H), **f32) if fused else None
+        planes = torch.empty((max(K - 1, 1), T, R, H), **f32) if fused and not cell.seq else None
         basis_h = None if fused else torch.empty((T, R, H * K), **f32)
         gh = None if fused else torch.empty((N, M, 4 * H), **f32)
-        if cell.seq:  # all T steps in one launch
+        if cell.seq:
+            # all T steps in one launch.  The h basis of every step as K planes
+            # [K][T+1][R][H] of one buffer: plane 0 at t = h_{t-1} (hs IS
+            # plane 0 shifted by one step, slot 0 = h0), planes k >= 1 written
+            # by the kernel -- so the h-weight gradient is ONE planes-layout
+            # GEMM over all orders and steps
+            hp = torch.empty((K, T + 1, R, H), **f32)
+            if not zero_init:
+                hp[0, 0].copy_(h0.reshape(R, H))
+            hs = hp[0, 1:].view(T, N, M, H)
+            planes = hp
             ops.lstm_seq_forward(plan, gx, Wh, b, K, T, N, gates, h0=None if zero_init else h0,
                                  c0=None if zero_init else c0, out_hs=hs, out_cs=cs, out_act=act,
-                                 planes=planes[0], plane_stride=T * R * H)
+                                 planes=hp[1] if K > 1 else None, plane_stride=(T + 1) * R * H)
         for t in range(0 if cell.seq else T):
             h_prev = (None if zero_init else h0) if t == 0 else hs[t - 1]
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
@@ -299,6 +309,9 @@ class _Layer(torch.autograd.Function):
                 dh_rec = None
         if T <= t_first:
             dWh = torch.zeros_like(Wh)
+        elif cell.seq:  # one GEMM over the K planes of every step with an h-conv
+            dWh = ops.weight_grad_planes(hb[0, t_first:T].reshape(-1, H), (T + 1) * R * H, K,
+                                         (T - t_first) * R, dpre[t_first:])
         elif fused:
             t0_parts, dparts = [], []
             if t_first == 0:  # step 0 ran its h-conv on h0

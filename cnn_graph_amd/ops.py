@@ -462,6 +462,33 @@ def weight_grad(basis: torch.Tensor, dy: torch.Tensor, out: torch.Tensor | None 
     return out
 
 
+def weight_grad_planes(planes: torch.Tensor, plane_stride: int, K: int, R: int, dy: torch.Tensor,
+                       out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
+    """dW [Fin*K, Fout] (row fin*K + k) = sum_k planes_k^T dy over R rows, the K
+    planes [R, Fin] of ``planes``' storage plane_stride floats apart (plane k
+    at planes.data_ptr() + k*plane_stride floats); one pass over dy."""
+    _check_dev("planes", planes)
+    _check_dev("dy", dy)
+    Fin = int(planes.shape[-1])
+    Fout = int(dy.shape[-1])
+    if dy.numel() != R * Fout or not dy.is_contiguous():
+        raise ValueError(f"dy must be a contiguous tensor of R*Fout = {R * Fout} elements")
+    avail = planes.untyped_storage().nbytes() // 4 - planes.storage_offset()
+    if plane_stride < R * Fin or avail < (K - 1) * plane_stride + R * Fin:
+        raise ValueError("planes: storage too small for K planes at this stride")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate=True needs an out tensor")
+        out = torch.empty((Fin * K, Fout), device=planes.device, dtype=torch.float32)
+    _check_out("out", out, (Fin * K, Fout))
+    nb = ctypes.c_size_t()
+    _lib.call("cg_weight_grad_workspace_bytes", R, Fin * K, Fout, ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 1), device=planes.device, dtype=torch.uint8)
+    _lib.call("cg_weight_grad_planes", int(R), Fin, int(K), Fout, _p(planes), int(plane_stride),
+              _p(dy), _p(out), int(accumulate), _p(ws), nb.value, _stream(planes))
+    return out
+
+
 def bias_grad(dy: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):
     """db = dy summed over every axis but the last (gradient of a broadcast bias)."""
     _check_dev("dy", dy)
@@ -618,6 +645,9 @@ def lstm_seq_forward(plan: ChebPlan, gx, Wh, bias, K: int, T: int, N: int, gates
     _check_out("cs", cs, (R, H))
     if out_act is not None:
         _check_out("act", out_act, (R, 4 * H))
+    if planes is None and K > 1:  # the kernel hands Chebyshev orders through them
+        planes = torch.empty((K - 1, R, H), **f32)
+        plane_stride = R * H
     if planes is not None:
         _check_dev("planes", planes)
         need = (K - 2) * plane_stride + R * H if K > 1 else 0

@@ -224,6 +224,14 @@ int cg_stack_merge_backward(int32_t N, int32_t M, int32_t F, const float* dy, co
 int cg_weight_grad_workspace_bytes(int64_t R, int32_t FinK, int32_t Fout, size_t* bytes);
 int cg_weight_grad(int64_t R, int32_t FinK, int32_t Fout, const float* basis, const float* dy,
                    float* dW, int32_t accumulate, void* workspace, size_t ws_bytes, void* stream);
+/* The same for a basis in the planes layout: K planes [R][Fin] plane_stride
+ * floats apart (plane k = T_k), dW [Fin*K][Fout] in the row order fin*K + k
+ * (lib/graph_conv.py:174); workspace as cg_weight_grad_workspace_bytes(R,
+ * Fin*K, Fout).  One pass over dy for all K orders (the gconv-LSTM's h-weight
+ * gradient summed over every time step). */
+int cg_weight_grad_planes(int64_t R, int32_t Fin, int32_t K, int32_t Fout, const float* planes,
+                          int64_t plane_stride, const float* dy, float* dW, int32_t accumulate,
+                          void* workspace, size_t ws_bytes, void* stream);
 /* db[c] (+)= sum_r dy[r][c] -- gradient of a broadcast bias add, dy [R][C]. */
 int cg_bias_grad_workspace_bytes(int64_t R, int32_t C, size_t* bytes);
 int cg_bias_grad(int64_t R, int32_t C, const float* dy, float* db, int32_t accumulate,
@@ -324,8 +332,10 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
  *   gx [T][N][M][4H]  the x-conv of every step (chebyshev5 of the [T*N] batch)
  *   h0, c0 [N][M][H]  initial state, NULL = zero state (step 0 then has no h-conv)
  *   hs, cs [T][N][M][H] OUT: h_t and c_t;  act [T][N][M][4H] OUT (nullable):
- *   gate activations z|i|f|o;  planes (nullable): T_k of h_{t-1} for
- *   k = 1..K-1 at (k-1)*plane_stride + [T][N][M][H] (steps with an h-conv only)
+ *   gate activations z|i|f|o;  planes (required for K > 1): T_k of h_{t-1} for
+ *   k = 1..K-1 at (k-1)*plane_stride + [T][N][M][H] (steps with an h-conv
+ *   only; each workgroup computes the orders of its own 16 channels and reads
+ *   its partner's from here)
  *   workspace: cg_lstm_seq_workspace_bytes (step counters + a status word).
  * cg_lstm_seq_status: waits for the stream, returns CG_ERR_HIP if a pair
  *   hand-off timed out (the launch then ends early instead of hanging).
