@@ -343,15 +343,17 @@ hipError_t launch_lstm_hstep(int gates, int N, int M, int K, const int* rowptr, 
                              hipStream_t s);
 // The gconv-LSTM layer forward over all T steps in ONE cooperative launch and
 // the BPTT step in one launch (lstm_seq.hip).  H == 32, M <= 1024.
-size_t lstm_seq_lds(int M, int K, int64_t nnz);
-bool lstm_seq_ok(int M, int H, int K, int64_t nnz);
+// xfin: feat_in of a fused x-conv (0: gx precomputed)
+size_t lstm_seq_lds(int M, int K, int64_t nnz, int xfin);
+bool lstm_seq_ok(int M, int H, int K, int64_t nnz, int xfin = 0);
 size_t lstm_bstep_lds(int M, int K, int64_t nnzT);
 bool lstm_bstep_ok(int M, int H, int K, int64_t nnzT);
 // workgroup pairs of the persistent forward (min(N, CUs / 2))
 int lstm_seq_pairs(int N, int device);
 // flags: 2P + 1 ints (pair step counters, then the status word), zeroed here
 hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, const int* rowptr,
-                           const int* col, const float* val, const int* order, const float* gx, const float* Wh,
+                           const int* col, const float* val, const int* order, const float* xs,
+                           const float* Wx, int Fin, float* xplanes, int64_t xpstride, const float* gx, const float* Wh,
                            const float* bias, const float* h0, const float* c0, float* hs,
                            float* cs, float* act, float* planes, int64_t pstride, int* flags,
                            int* status, int P, hipStream_t s);

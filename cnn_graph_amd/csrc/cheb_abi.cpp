@@ -1465,21 +1465,32 @@ int cg_lstm_seq_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* su
   return ok();
 }
 
+int cg_lstm_seq_x_supported(const cg_plan* plan, int32_t Fin, int32_t H, int32_t K, int32_t* supported) {
+  if (!plan || !supported) return fail(CG_ERR_ARG, "lstm_seq_x_supported: null argument");
+  *supported = (Fin >= 1 && Fin <= 8 && cg::lstm_seq_ok(plan->M, H, K, plan->nnz, Fin) &&
+                cg::lstm_bstep_ok(plan->M, H, K, plan->nnzT)) ? 1 : 0;
+  return ok();
+}
+
 int cg_lstm_seq_workspace_bytes(const cg_plan* plan, int32_t N, size_t* bytes) {
   if (!plan || !bytes || N < 1) return fail(CG_ERR_ARG, "lstm_seq_workspace_bytes: bad arguments");
   *bytes = al256(sizeof(int) * (size_t(2) * cg::lstm_seq_pairs(N, plan->device) + 1));
   return ok();
 }
 
-int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t K, int32_t gates,
-                        const float* gx, const float* Wh, const float* bias, const float* h0,
-                        const float* c0, float* hs, float* cs, float* act, float* planes,
-                        int64_t plane_stride, void* workspace, size_t ws_bytes, void* stream) {
+static int lstm_seq_impl(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t K, int32_t gates,
+                         const float* gx, const float* xs, const float* Wx, int32_t Fin,
+                         float* xplanes, int64_t xplane_stride, const float* Wh, const float* bias,
+                         const float* h0, const float* c0, float* hs, float* cs, float* act,
+                         float* planes, int64_t plane_stride, void* workspace, size_t ws_bytes,
+                         void* stream) {
   int rc = check_lstm(int64_t(T) * N * (plan ? plan->M : 1), H, gates);
   if (rc) return rc;
   if (!plan || T < 1 || N < 1 || K < 1) return fail(CG_ERR_ARG, "lstm_seq_forward: bad plan / T / N / K");
-  if (!gx || !Wh || !hs || !cs) return fail(CG_ERR_ARG, "lstm_seq_forward: null gx / Wh / hs / cs");
-  if (!cg::lstm_seq_ok(plan->M, H, K, plan->nnz))
+  if ((!gx && !xs) || !Wh || !hs || !cs) return fail(CG_ERR_ARG, "lstm_seq_forward: null gx|xs / Wh / hs / cs");
+  if (xs && (Fin < 1 || Fin > 8 || !Wx || !xplanes))
+    return fail(CG_ERR_ARG, "lstm_seq_forward_x: needs 1 <= feat_in <= 8, Wx and the x planes");
+  if (!cg::lstm_seq_ok(plan->M, H, K, plan->nnz, xs ? Fin : 0))
     return fail(CG_ERR_UNSUPPORTED, "lstm_seq_forward: needs H = 32, M <= 1024 and L~ plus the "
                                     "weights in LDS (M=%d nnz=%lld H=%d K=%d)",
                 plan->M, (long long)plan->nnz, H, K);
@@ -1489,13 +1500,16 @@ int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t 
                             "its quarters' Chebyshev orders to the partner through them)");
   if (planes && K > 1 && plane_stride < R * H)
     return fail(CG_ERR_ARG, "lstm_seq_forward: plane stride %lld < T*N*M*H", (long long)plane_stride);
-  if (!al16(gx) || !al16(hs) || !al16(cs) || (act && !al16(act)) || (planes && !al16(planes)) ||
+  if (xs && xplane_stride < R * Fin)
+    return fail(CG_ERR_ARG, "lstm_seq_forward_x: x plane stride %lld < T*N*M*feat_in",
+                (long long)xplane_stride);
+  if ((gx && !al16(gx)) || !al16(hs) || !al16(cs) || (act && !al16(act)) || (planes && !al16(planes)) ||
       (h0 && !al16(h0)) || (c0 && !al16(c0)) || (bias && !al16(bias)) ||
       (planes && K > 1 && (plane_stride & 3)))
     return fail(CG_ERR_ARG, "lstm_seq_forward: tensors must be 16-byte aligned (float4 access), "
                             "plane stride a multiple of 4");
-  const void* outs[] = {hs, cs, act, planes};
-  const void* ins[] = {gx, Wh, bias, h0, c0};
+  const void* outs[] = {hs, cs, act, planes, xplanes};
+  const void* ins[] = {gx, xs, Wx, Wh, bias, h0, c0};
   for (const void* o : outs)
     for (const void* i : ins)
       if (o && o == i) return fail(CG_ERR_ARG, "lstm_seq_forward: outputs must not alias inputs");
@@ -1507,9 +1521,29 @@ int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t 
   const int P = cg::lstm_seq_pairs(N, plan->device);
   int* flags = static_cast<int*>(workspace);
   CG_HIP(cg::launch_lstm_seq(gates, T, N, plan->M, K, plan->nnz, plan->rowptr, plan->col, plan->val,
-                             plan->lorder, gx, Wh, bias, h0, c0, hs, cs, act, planes, plane_stride, flags,
-                             flags + 2 * P, P, reinterpret_cast<hipStream_t>(stream)));
+                             plan->lorder, xs, Wx, Fin, xplanes, xplane_stride, gx, Wh, bias, h0,
+                             c0, hs, cs, act, planes, plane_stride, flags, flags + 2 * P, P,
+                             reinterpret_cast<hipStream_t>(stream)));
   return ok();
+}
+
+int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t K, int32_t gates,
+                        const float* gx, const float* Wh, const float* bias, const float* h0,
+                        const float* c0, float* hs, float* cs, float* act, float* planes,
+                        int64_t plane_stride, void* workspace, size_t ws_bytes, void* stream) {
+  return lstm_seq_impl(plan, T, N, H, K, gates, gx, nullptr, nullptr, 0, nullptr, 0, Wh, bias, h0,
+                       c0, hs, cs, act, planes, plane_stride, workspace, ws_bytes, stream);
+}
+
+int cg_lstm_seq_forward_x(cg_plan* plan, int32_t T, int32_t N, int32_t Fin, int32_t H, int32_t K,
+                          int32_t gates, const float* xs, const float* Wx, float* xplanes,
+                          int64_t xplane_stride, const float* Wh, const float* bias,
+                          const float* h0, const float* c0, float* hs, float* cs, float* act,
+                          float* planes, int64_t plane_stride, void* workspace, size_t ws_bytes,
+                          void* stream) {
+  if (!xs) return fail(CG_ERR_ARG, "lstm_seq_forward_x: null xs");
+  return lstm_seq_impl(plan, T, N, H, K, gates, nullptr, xs, Wx, Fin, xplanes, xplane_stride, Wh,
+                       bias, h0, c0, hs, cs, act, planes, plane_stride, workspace, ws_bytes, stream);
 }
 
 int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,

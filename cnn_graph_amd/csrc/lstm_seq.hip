@@ -3,8 +3,9 @@
 // (lib/gconv_lstm.py:609-627 glstm_layer -> static_rnn over GConvLSTMCell,
 // :77-221), H = 32 hidden units, M <= 1024 vertices.
 //
-// Per time step the cell computes (x-conv gx precomputed for all steps at
-// once by the time-batched chebyshev5 call):
+// Per time step the cell computes (the x-conv either fused in -- feat_in <= 8:
+// the recurrence of x_t in the same LDS slots, Wx on the same MFMAs -- or
+// precomputed for all steps at once by the time-batched chebyshev5 call, gx):
 //   T_0 = h, T_1 = L~ h, T_k = 2 L~ T_{k-1} - T_{k-2}       (cheby_conv, :183-207)
 //   a = (gx + sum_k T_k Wh_k) + b
 //   z = tan(a_z), i = sigmoid(a_i), f = sigmoid(a_f), o = tanh(a_o)   (reference)
@@ -97,7 +98,12 @@ struct SeqArgs {
   const float* val;
   const int* order;   // rows by decreasing length (lane -> row)
   int M, Mr, K, N, T, gates, nnz, P, pair_xcd;
-  const float* gx;    // [T][N][M][128] x-conv gate pre-activations
+  const float* gx;    // [T][N][M][128] x-conv gate pre-activations (when xs == NULL)
+  const float* xs;    // [T][N][M][Fin] inputs, Fin <= 8: the x-conv fused in (gx unused)
+  const float* Wx;    // [K*Fin][128], row fin*K + k (with xs)
+  float* xplanes;     // T_k of x_t, k = 0..K-1 at k*xpstride + [T][N][M][Fin] (with xs)
+  int64_t xpstride;
+  int Fin;
   const float* Wh;    // [K*32][128], row c*K + k
   const float* bias;  // [128] or NULL
   const float* h0;    // [N][M][32] or NULL (zero state: step 0 has no h-conv)
@@ -134,7 +140,8 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
   float* slot0 = smem;
   float* slot1 = smem + A.Mr * kQ;
   float* s_W = slot1 + A.Mr * kQ;  // [K][q 4][s 4][hh 2][ct 2][i 32]
-  float* s_b = s_W + K * 2048;  // [128] bias (zeros when NULL)
+  float* s_Wx = s_W + K * 2048;  // [K][s 4][hh 2][ct 2][i 32] x-conv A operands (xs != NULL)
+  float* s_b = s_Wx + (A.xs ? K * 512 : 0);  // [128] bias (zeros when NULL)
   float* s_val = s_b + 128;
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
   // A operands of the transposed contraction: lane (i, hh) of MFMA step s in
@@ -146,6 +153,15 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
     const int ch = 8 * q + 4 * h2 + s;
     const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
     s_W[e] = A.Wh[int64_t(ch * K + k) * 128 + gcol];
+  }
+  if (A.xs) {
+    // x channel c = 4hh + s of MFMA step s (zero past Fin)
+    for (int e = tid; e < K * 512; e += kST) {
+      const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3, k = e >> 9;
+      const int c = 4 * h2 + s;
+      const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
+      s_Wx[e] = c < A.Fin ? A.Wx[int64_t(c * K + k) * 128 + gcol] : 0.f;
+    }
   }
   for (int e = tid; e < 128; e += kST) s_b[e] = A.bias ? A.bias[e] : 0.f;
   for (int e = tid; e < A.nnz; e += kST) {
@@ -195,8 +211,8 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
       float* pl_t = A.planes + (int64_t(t) * N + n) * M * kH;  // plane k at + (k-1)*pstride
       // gates^T += Wh_k^T T_k^T over quarter q's 8 channels; B operand: the
       // lane's own rows of T_k (tk, channels 8q + 4hh .. +3)
-      auto contract = [&](int q, int k, const float4* tk) {
-        const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
+      auto contract = [&](int q, int k, const float4* tk) {  // q = 4: the x quarter
+        const float* wq = (q < 4 ? s_W + (k * 4 + q) * 512 : s_Wx + k * 512) + hh * 64 + j;
 #pragma unroll
         for (int s = 0; s < 4 && !CG_DBG(A.dbg, 1); ++s) {
           const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
@@ -208,6 +224,64 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           }
         }
       };
+      if (A.xs) {
+        // the fused x-conv: the recurrence of x_t (Fin <= 8 channels in one
+        // 8-channel slot, the rest zero) and its contraction with Wx; both
+        // workgroups run it, workgroup 0 keeps the x basis planes
+        const int Fin = A.Fin;
+        const float* xt = A.xs + (int64_t(t) * N + n) * M * Fin;
+        float* xp = A.xplanes + (int64_t(t) * N + n) * M * Fin;
+#pragma unroll
+        for (int rt = 0; rt < kRT; ++rt) {
+          if (!rvS[rt]) continue;
+          float v[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int ch = 4 * hs2 + c;
+            v[c] = ch < Fin ? xt[int64_t(rowS[rt]) * Fin + ch] : 0.f;
+            if (ch < Fin && u == 0) xp[int64_t(rowS[rt]) * Fin + ch] = v[c];
+          }
+          *reinterpret_cast<float4*>(slot0 + rowS[rt] * kQ + 4 * hs2) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+        __syncthreads();
+        for (int k = 0; k < K; ++k) {
+          const float* cur = (k & 1) ? slot1 : slot0;
+          float4 tk[kRT];
+#pragma unroll
+          for (int rt = 0; rt < kRT; ++rt)
+            tk[rt] = *reinterpret_cast<const float4*>(cur + row[rt] * kQ + 4 * hh);
+          contract(4, k, tk);
+          if (k + 1 < K) {
+            float* nxt = (k & 1) ? slot0 : slot1;
+#pragma unroll
+            for (int rt = 0; rt < kRT; ++rt) {
+              if (!rvS[rt]) continue;
+              if (4 * hs2 >= Fin) {  // channels past Fin stay zero
+                *reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2) = make_float4(0.f, 0.f, 0.f, 0.f);
+                continue;
+              }
+              float4 sm;
+              with_row_len(wl[rt], [&](auto lc) {
+                sm = lds_row_spmm<decltype(lc)::value>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
+              });
+              float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2);
+              if (k >= 1) {
+                const float4 p = *own;
+                sm = make_float4(2.f * sm.x - p.x, 2.f * sm.y - p.y, 2.f * sm.z - p.z, 2.f * sm.w - p.w);
+              }
+              *own = sm;
+              if (u == 0) {
+                float* dst = xp + int64_t(k + 1) * A.xpstride + int64_t(rowS[rt]) * Fin;
+                const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                  if (4 * hs2 + c < Fin) dst[4 * hs2 + c] = sv[c];
+              }
+            }
+            __syncthreads();
+          }
+        }
+      }
       if (has_h) {
         // the two OWN quarters (units 16u .. 16u+15): the recurrence in LDS,
         // T_1 .. T_{K-1} leave as basis planes (write-through: the partner reads them)
@@ -316,8 +390,8 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           float4 gv[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            gv[g] = CG_DBG(A.dbg, 16) ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                      : *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
+            gv[g] = (CG_DBG(A.dbg, 16) || A.xs) ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                                : *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
           // c_{t-1}: this lane's own store of the previous step (same address,
           // same lane), or the initial state
           float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -595,14 +669,15 @@ inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 }  // namespace
 
-size_t lstm_seq_lds(int M, int K, int64_t nnz) {
-  return size_t(2) * round_up(M + 1, 32) * kQ * 4 + size_t(K) * 2048 * 4 + 512 + size_t(nnz) * 4 +
+size_t lstm_seq_lds(int M, int K, int64_t nnz, int xfin) {
+  return size_t(2) * round_up(M + 1, 32) * kQ * 4 + size_t(K) * 2048 * 4 +
+         (xfin > 0 ? size_t(K) * 512 * 4 : 0) + 512 + size_t(nnz) * 4 +
          align16(size_t(nnz) * 2);
 }
 
-bool lstm_seq_ok(int M, int H, int K, int64_t nnz) {
-  return H == kH && M >= 1 && M <= kRT * 8 * 32 && K >= 1 && nnz >= 1 &&
-         lstm_seq_lds(M, K, nnz) <= size_t(kLdsBytes - kSeqStaticLds);
+bool lstm_seq_ok(int M, int H, int K, int64_t nnz, int xfin) {
+  return H == kH && M >= 1 && M <= kRT * 8 * 32 && K >= 1 && nnz >= 1 && xfin <= 8 &&
+         lstm_seq_lds(M, K, nnz, xfin) <= size_t(kLdsBytes - kSeqStaticLds);
 }
 
 size_t lstm_bstep_lds(int M, int K, int64_t nnzT) {
@@ -625,11 +700,13 @@ int lstm_seq_pairs(int N, int device) {
 }
 
 hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, const int* rowptr,
-                           const int* col, const float* val, const int* order, const float* gx, const float* Wh,
+                           const int* col, const float* val, const int* order, const float* xs,
+                           const float* Wx, int Fin, float* xplanes, int64_t xpstride, const float* gx, const float* Wh,
                            const float* bias, const float* h0, const float* c0, float* hs,
                            float* cs, float* act, float* planes, int64_t pstride, int* flags,
                            int* status, int P, hipStream_t s) {
-  if (!lstm_seq_ok(M, kH, K, nnz) || N < 1 || T < 1 || P < 1 || P > N)
+  if (!lstm_seq_ok(M, kH, K, nnz, xs ? Fin : 0) || N < 1 || T < 1 || P < 1 || P > N ||
+      (xs && (Fin < 1 || Fin > 8 || !Wx || !xplanes)) || (!xs && !gx))
     return hipErrorInvalidValue;
   // the kernel's static LDS (the abort word) counts against the same 160 KB
   static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_seq),
@@ -642,7 +719,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
       rate_khz <= 0)
     rate_khz = 100000;  // 100 MHz
   SeqArgs a{rowptr, col, val, order, M, round_up(M + 1, 32), K, N, T, gates, int(nnz), P,
-            P % 8 == 0 ? 1 : 0, gx, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
+            P % 8 == 0 ? 1 : 0, gx, xs, Wx, xplanes, xpstride, Fin, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
             // a pair hand-off that has not happened after 2 s ends the launch
             static_cast<unsigned long long>(rate_khz) * 2000ull, (debug_flags() >> 16) & 0xff,
             nullptr};
@@ -655,7 +732,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   // resident at once: check the grid against the occupancy query (what a
   // cooperative launch would check, MI355X_MICROARCH.md §Residency), with one
   // workgroup per CU of margin, then launch plainly
-  const size_t lds = lstm_seq_lds(M, K, nnz);
+  const size_t lds = lstm_seq_lds(M, K, nnz, xs ? Fin : 0);
   int per_cu = 0, cus = 0;
   e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_lstm_seq),
                                                    kST, lds);

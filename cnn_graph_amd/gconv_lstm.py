@@ -107,6 +107,8 @@ class GConvLSTMCell:
             raise ValueError(f"hconv='seq' needs H = 32, M <= 1024, K <= 4 and L~ in LDS "
                              f"(H={H}, M={self.plan.M}, K={self._K})")
         self.seq = seq_ok and hconv in ("auto", "seq")
+        # feat_in <= 8: the x-conv runs inside the sequence kernel too
+        self.seq_x = self.seq and ops.lstm_seq_x_supported(self.plan, self._feat_in, H, self._K)
         self.fused = supported and hconv != "unfused"
 
     # -- reference properties ---------------------------------------------------
@@ -235,9 +237,12 @@ class _Layer(torch.autograd.Function):
         R = N * M
         dev = xs.device
         f32 = dict(device=dev, dtype=torch.float32)
-        # x-conv of every step at once: a batch of T*N samples
-        basis_x, gx = ops.cheb_forward(plan, xs.view(T * N, M, F), Wx, K)
-        gx = gx.view(T, R, 4 * H)
+        seq_x = cell.seq and cell.seq_x
+        if seq_x:  # the x-conv inside the sequence kernel; its basis kept as planes
+            basis_x, gx = torch.empty((K, T * R, F), device=dev, dtype=torch.float32), None
+        else:  # x-conv of every step at once: a batch of T*N samples
+            basis_x, gx = ops.cheb_forward(plan, xs.view(T * N, M, F), Wx, K)
+            gx = gx.view(T, R, 4 * H)
         hs = torch.empty((T, N, M, H), **f32)
         cs = torch.empty((T, N, M, H), **f32)
         act = torch.empty((T, R, 4 * H), **f32)
@@ -258,9 +263,16 @@ class _Layer(torch.autograd.Function):
                 hp[0, 0].copy_(h0.reshape(R, H))
             hs = hp[0, 1:].view(T, N, M, H)
             planes = hp
-            ops.lstm_seq_forward(plan, gx, Wh, b, K, T, N, gates, h0=None if zero_init else h0,
-                                 c0=None if zero_init else c0, out_hs=hs, out_cs=cs, out_act=act,
-                                 planes=hp[1] if K > 1 else None, plane_stride=(T + 1) * R * H)
+            if seq_x:
+                ops.lstm_seq_forward_x(plan, xs, Wx, Wh, b, K, gates, h0=None if zero_init else h0,
+                                       c0=None if zero_init else c0, out_hs=hs, out_cs=cs,
+                                       out_act=act, planes=hp[1] if K > 1 else None,
+                                       plane_stride=(T + 1) * R * H, xplanes=basis_x)
+            else:
+                ops.lstm_seq_forward(plan, gx, Wh, b, K, T, N, gates, h0=None if zero_init else h0,
+                                     c0=None if zero_init else c0, out_hs=hs, out_cs=cs,
+                                     out_act=act, planes=hp[1] if K > 1 else None,
+                                     plane_stride=(T + 1) * R * H)
         for t in range(0 if cell.seq else T):
             h_prev = (None if zero_init else h0) if t == 0 else hs[t - 1]
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
@@ -275,6 +287,7 @@ class _Layer(torch.autograd.Function):
                                   out_c=cs[t], out_h=hs[t], out_act=act[t])
         ctx.save_for_backward(basis_x, planes if fused else basis_h, Wx, Wh, act, cs, c0, h0, hs)
         ctx.cell, ctx.zero_init, ctx.shape, ctx.fused = cell, zero_init, (T, N, M, F), fused
+        ctx.seq_x = seq_x
         return hs, cs[T - 1].clone()
 
     @staticmethod
@@ -324,8 +337,15 @@ class _Layer(torch.autograd.Function):
                                        H, K)
         else:
             dWh = ops.weight_grad(hb[t_first:], dpre[t_first:])
-        dxs, dWx = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), basis_x, Wx, K,
-                                     need_dx=ctx.needs_input_grad[0])
+        if ctx.seq_x:  # the x basis as K planes [T*R][F]: one planes GEMM; dx needs no basis
+            dWx = ops.weight_grad_planes(basis_x[0], T * R * F, K, T * R, dpre)
+            dxs = None
+            if ctx.needs_input_grad[0]:
+                dxs, _ = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), None, Wx, K,
+                                           need_dW=False)
+        else:
+            dxs, dWx = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), basis_x, Wx, K,
+                                         need_dx=ctx.needs_input_grad[0])
         db = ops.bias_grad(dpre)
         dx_out = dxs.view(T, N, M, F) if dxs is not None else None
         dc0 = None if zero_init else dc

@@ -668,6 +668,60 @@ def lstm_seq_forward(plan: ChebPlan, gx, Wh, bias, K: int, T: int, N: int, gates
     return hs, cs, out_act
 
 
+def lstm_seq_x_supported(plan: ChebPlan, Fin: int, H: int, K: int) -> bool:
+    """Whether cg_lstm_seq_forward_x (the x-conv fused in) serves feat_in = Fin."""
+    ok = ctypes.c_int32()
+    _lib.call("cg_lstm_seq_x_supported", plan.handle, int(Fin), int(H), int(K), ctypes.byref(ok))
+    return bool(ok.value)
+
+
+def lstm_seq_forward_x(plan: ChebPlan, xs, Wx, Wh, bias, K: int, gates="reference", h0=None,
+                       c0=None, out_hs=None, out_cs=None, out_act=None, planes=None,
+                       plane_stride: int = 0, xplanes=None, check: bool = False):
+    """lstm_seq_forward with the x-conv fused in (cg_lstm_seq_forward_x; feat_in
+    <= 8): xs [T, N, M, F] instead of gx.  xplanes (optional, [K, T, N*M, F]):
+    receives the x basis T_k(x_t), k = 0..K-1.  Returns (hs, cs, act, xplanes)."""
+    _check_dev("xs", xs)
+    xs = xs.contiguous()
+    T, N, M, F = (int(v) for v in xs.shape)
+    H = int(Wh.shape[1]) // 4
+    R = T * N * M
+    dev = xs.device
+    f32 = dict(device=dev, dtype=torch.float32)
+    if tuple(Wx.shape) != (K * F, 4 * H) or not Wx.is_contiguous():
+        raise ValueError(f"Wx must be a contiguous [{K * F}, {4 * H}] tensor")
+    if tuple(Wh.shape) != (K * H, 4 * H) or not Wh.is_contiguous():
+        raise ValueError(f"Wh must be a contiguous [{K * H}, {4 * H}] tensor")
+    for name, t, n in (("bias", bias, 4 * H), ("h0", h0, N * M * H), ("c0", c0, N * M * H)):
+        if t is not None:
+            _check_dev(name, t)
+            if not t.is_contiguous() or t.numel() != n or t.data_ptr() % 16:
+                raise ValueError(f"{name}: need a contiguous 16-byte aligned tensor of {n} floats")
+    hs = out_hs if out_hs is not None else torch.empty((T, N, M, H), **f32)
+    cs = out_cs if out_cs is not None else torch.empty((T, N, M, H), **f32)
+    _check_out("hs", hs, (R, H))
+    _check_out("cs", cs, (R, H))
+    if out_act is not None:
+        _check_out("act", out_act, (R, 4 * H))
+    if planes is None and K > 1:
+        planes = torch.empty((K - 1, R, H), **f32)
+        plane_stride = R * H
+    if xplanes is None:
+        xplanes = torch.empty((K, R, F), **f32)
+    _check_out("xplanes", xplanes, (K * R * F,))
+    nb = ctypes.c_size_t()
+    _lib.call("cg_lstm_seq_workspace_bytes", plan.handle, int(N), ctypes.byref(nb))
+    ws = torch.empty(int(nb.value), device=dev, dtype=torch.uint8)
+    s = _stream(xs)
+    _lib.call("cg_lstm_seq_forward_x", plan.handle, T, N, F, int(H), int(K), LSTM_GATES[gates],
+              _p(xs), _p(Wx), _p(xplanes), R * F, _p(Wh), _p(bias), _p(h0), _p(c0), _p(hs), _p(cs),
+              _p(out_act), _p(planes), int(plane_stride), _p(ws), int(nb.value), s)
+    if check:
+        st = ctypes.c_int32()
+        _lib.call("cg_lstm_seq_status", plan.handle, int(N), _p(ws), ctypes.byref(st), s)
+    return hs, cs, out_act, xplanes
+
+
 def lstm_bwd_step(plan: ChebPlan, dh, dh_rec, dc, act, c_prev, c_out, Wh, K: int,
                   gates="reference", out_dpre=None, need_dc_prev=True, out_dh_prev=None):
     """One BPTT step of a gconv-LSTM layer in ONE launch (cg_lstm_bwd_step):

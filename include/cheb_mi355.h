@@ -350,6 +350,17 @@ int cg_lstm_seq_forward(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t 
                         const float* gx, const float* Wh, const float* bias, const float* h0,
                         const float* c0, float* hs, float* cs, float* act, float* planes,
                         int64_t plane_stride, void* workspace, size_t ws_bytes, void* stream);
+/* The same with the x-conv fused in (feat_in <= 8): xs [T][N][M][Fin] instead of
+ * gx, Wx [K*Fin][4H] (row fin*K + k); xplanes OUT: the x basis T_k(x_t),
+ * k = 0..K-1, at k*xplane_stride + [T][N][M][Fin] (the backward's dWx). */
+int cg_lstm_seq_x_supported(const cg_plan* plan, int32_t Fin, int32_t H, int32_t K,
+                            int32_t* supported);
+int cg_lstm_seq_forward_x(cg_plan* plan, int32_t T, int32_t N, int32_t Fin, int32_t H, int32_t K,
+                          int32_t gates, const float* xs, const float* Wx, float* xplanes,
+                          int64_t xplane_stride, const float* Wh, const float* bias,
+                          const float* h0, const float* c0, float* hs, float* cs, float* act,
+                          float* planes, int64_t plane_stride, void* workspace, size_t ws_bytes,
+                          void* stream);
 int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,
                        void* stream);
 int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,

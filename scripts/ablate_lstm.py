@@ -46,14 +46,27 @@ def main():
     h.cg_debug_set_flags.argtypes = [ctypes.c_int]
     h.cg_debug_set_ts.argtypes = [ctypes.c_void_p]
 
+    Fin = 2
+    xs = torch.rand((T, N, M, Fin), device=dev, generator=g)
+    Wx = torch.randn((K * Fin, 4 * H), device=dev, generator=g) * 0.1
+    xpl = torch.empty((K, T * N * M, Fin), device=dev)
+    mode = {"x": False}
+
     def run():
-        ops.lstm_seq_forward(plan, gx, Wh, b, K, T, N, out_hs=hs, out_cs=cs, out_act=act,
-                             planes=planes[0], plane_stride=T * N * M * H)
+        if mode["x"]:
+            ops.lstm_seq_forward_x(plan, xs, Wx, Wh, b, K, out_hs=hs, out_cs=cs, out_act=act,
+                                   planes=planes[0], plane_stride=T * N * M * H, xplanes=xpl)
+        else:
+            ops.lstm_seq_forward(plan, gx, Wh, b, K, T, N, out_hs=hs, out_cs=cs, out_act=act,
+                                 planes=planes[0], plane_stride=T * N * M * H)
 
     out = {}
     buf = torch.zeros((256, 8), dtype=torch.int64, device=dev)
+    sets = [(nm, fl, False) for nm, fl in SETS.items()] + \
+        [("x_" + nm, fl, True) for nm, fl in SETS.items() if nm in ("full", "no_loads", "nothing")]
     for rnd in range(3):
-        for name, fl in SETS.items():
+        for name, fl, xm in sets:
+            mode["x"] = xm
             h.cg_debug_set_flags(fl << 16)
             run()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
