@@ -92,6 +92,32 @@ __device__ __forceinline__ void st16_sc1(float* p, float4 v) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 16-byte agent-scope accesses as buffer_load/store_dwordx4 ... sc1 (aux 16)
+// through a descriptor over one [M][32] slab; the 8-byte forms above move
+// 0.54-0.70x the bytes per instruction (MI355X_MICROARCH.md fence table)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* p, int M) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, M * kH * 4, 0x00020000);
+}
+__device__ __forceinline__ float4 bld16_sc1(__amdgpu_buffer_rsrc_t r, int off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off * 4, 0, 16);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+__device__ __forceinline__ float4 bld16(__amdgpu_buffer_rsrc_t r, int off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off * 4, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+__device__ __forceinline__ void bst16_sc1(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+  u32x4 w;
+  w.x = __float_as_uint(v.x);
+  w.y = __float_as_uint(v.y);
+  w.z = __float_as_uint(v.z);
+  w.w = __float_as_uint(v.w);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off * 4, 0, 16);
+}
+
 struct SeqArgs {
   const int* rowptr;  // L~ (CSR, sorted columns)
   const int* col;
@@ -117,7 +143,8 @@ struct SeqArgs {
   int* status;        // [1] 0 = ok, 1 = a hand-off timed out
   unsigned long long timeout;  // wall-clock ticks
   int dbg;            // ablation build only (CG_DBG): 1 no MFMA, 2 no SpMM, 4 no gate math,
-                      // 8 no partner wait, 16 no gx / c loads, 32 no plane stores
+                      // 8 no partner wait, 16 no gx / c loads, 32 no plane stores,
+                      // 64 no act stores, 128 no c stores, 256 no h stores
   unsigned long long* ts;  // ablation build: phase stamps of step 1 (CG_TS), else NULL
 };
 
@@ -209,6 +236,8 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
       const float* hsrc = (t == 0) ? A.h0 + int64_t(n) * M * kH
                                    : A.hs + (int64_t(t - 1) * N + n) * M * kH;
       float* pl_t = A.planes + (int64_t(t) * N + n) * M * kH;  // plane k at + (k-1)*pstride
+      const __amdgpu_buffer_rsrc_t r_hsrc = slab_rsrc(hsrc, M);
+      const __amdgpu_buffer_rsrc_t r_hout = slab_rsrc(A.hs + (int64_t(t) * N + n) * M * kH, M);
       // gates^T += Wh_k^T T_k^T over quarter q's 8 channels; B operand: the
       // lane's own rows of T_k (tk, channels 8q + 4hh .. +3)
       auto contract = [&](int q, int k, const float4* tk) {  // q = 4: the x quarter
@@ -287,14 +316,18 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
         // T_1 .. T_{K-1} leave as basis planes (write-through: the partner reads them)
         for (int qq = 0; qq < 2; ++qq) {
           const int q = 2 * u + qq;
+          // all tiles' loads in flight together; a padding lane (row M) reads
+          // past the slab (the descriptor's range check returns 0) and
+          // rewrites the zero row with 0
+          float4 v[kRT];
 #pragma unroll
           for (int rt = 0; rt < kRT; ++rt) {
-            if (rv[rt]) {
-              const float* p = hsrc + int64_t(row[rt]) * kH + 8 * q + 4 * hh;
-              const float4 v = (t > 0) ? ld16_sc1(p) : *reinterpret_cast<const float4*>(p);
-              *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = v;
-            }
+            const int off = row[rt] * kH + 8 * q + 4 * hh;
+            v[rt] = (t > 0) ? bld16_sc1(r_hsrc, off) : bld16(r_hsrc, off);
           }
+#pragma unroll
+          for (int rt = 0; rt < kRT; ++rt)
+            *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = v[rt];
           __syncthreads();
           for (int k = 0; k < K; ++k) {
             const float* cur = (k & 1) ? slot1 : slot0;
@@ -325,7 +358,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
                 const float4 o = make_float4(s0, s1, s2, s3);
                 *own = o;
                 if (!CG_DBG(A.dbg, 32))
-                  st16_sc1(pl_t + int64_t(k) * A.pstride + int64_t(rowS[rt]) * kH + 8 * q + 4 * hs2, o);
+                  bst16_sc1(slab_rsrc(pl_t + int64_t(k) * A.pstride, M), rowS[rt] * kH + 8 * q + 4 * hs2, o);
               }
               __syncthreads();
             }
@@ -365,13 +398,12 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           const int q = 2 * (1 - u) + qq;
           for (int k = 0; k < K; ++k) {
             const float* src = (k == 0) ? hsrc : pl_t + int64_t(k - 1) * A.pstride;
+            const __amdgpu_buffer_rsrc_t r_src = slab_rsrc(src, M);
             float4 tk[kRT];
 #pragma unroll
-            for (int rt = 0; rt < kRT; ++rt) {
-              const float* p = src + int64_t(row[rt]) * kH + 8 * q + 4 * hh;
-              tk[rt] = !rv[rt] ? make_float4(0.f, 0.f, 0.f, 0.f)
-                               : (k == 0 && t == 0) ? *reinterpret_cast<const float4*>(p)
-                                                    : ld16_sc1(p);
+            for (int rt = 0; rt < kRT; ++rt) {  // row M: past the slab, reads 0
+              const int off = row[rt] * kH + 8 * q + 4 * hh;
+              tk[rt] = (k == 0 && t == 0) ? bld16(r_src, off) : bld16_sc1(r_src, off);
             }
             contract(q, k, tk);
           }
@@ -437,10 +469,12 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
             ff[m] = fg;
             oo[m] = o;
           }
-          *reinterpret_cast<float4*>(A.cs + rr * kH + u0) =
-              make_float4(c[0], c[1], c[2], c[3]);
-          st16_sc1(A.hs + rr * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
-          if (A.act) {
+          if (!CG_DBG(A.dbg, 128))
+            *reinterpret_cast<float4*>(A.cs + rr * kH + u0) =
+                make_float4(c[0], c[1], c[2], c[3]);
+          if (!CG_DBG(A.dbg, 256))
+            bst16_sc1(r_hout, row[rt] * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
+          if (A.act && !CG_DBG(A.dbg, 64)) {
             float* ap = A.act + rr * 128 + u0;
             *reinterpret_cast<float4*>(ap) = make_float4(zz[0], zz[1], zz[2], zz[3]);
             *reinterpret_cast<float4*>(ap + 32) = make_float4(ii[0], ii[1], ii[2], ii[3]);

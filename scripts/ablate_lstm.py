@@ -4,7 +4,7 @@
 build (`make debug`, loaded through CG_LIB_PATH; outputs are garbage when a
 flag is set -- timing only).  Flags (bits 16.. of cg_debug_set_flags): 1 no
 MFMA, 2 no SpMM, 4 no gate math, 8 no partner wait, 16 no gx / c loads,
-32 no plane stores.  Phase stamps (step 1, thread 0 of every workgroup, 100 MHz):
+32 no plane stores, 64 no act stores, 128 no c stores, 256 no h stores.  Phase stamps (step 1, thread 0 of every workgroup, 100 MHz):
 step start, own quarters done, partner wait done, all quarters done, epilogue +
 flag done -- median over workgroups, us from the step start."""
 import ctypes
@@ -23,7 +23,11 @@ from cnn_graph_amd import _lib, ops  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
 SETS = {"full": 0, "no_mfma": 1, "no_spmm": 2, "no_gate_math": 4, "no_wait": 8, "no_loads": 16,
-        "no_planes": 32, "no_mfma_spmm": 3, "only_epilogue": 1 | 2 | 32, "nothing": 63}
+        "no_planes": 32, "no_mfma_spmm": 3, "only_epilogue": 1 | 2 | 32, "nothing": 63,
+        "no_act": 64, "no_act_c": 64 | 128, "no_stores": 64 | 128 | 256 | 32,
+        "nothing_but_stores": 1 | 2 | 4 | 8 | 16}
+XSETS = ("full", "no_loads", "nothing", "no_act", "no_act_c", "no_stores", "no_wait",
+         "no_mfma_spmm", "nothing_but_stores")
 
 
 def main():
@@ -63,7 +67,7 @@ def main():
     out = {}
     buf = torch.zeros((256, 8), dtype=torch.int64, device=dev)
     sets = [(nm, fl, False) for nm, fl in SETS.items()] + \
-        [("x_" + nm, fl, True) for nm, fl in SETS.items() if nm in ("full", "no_loads", "nothing")]
+        [("x_" + nm, fl, True) for nm, fl in SETS.items() if nm in XSETS]
     for rnd in range(3):
         for name, fl, xm in sets:
             mode["x"] = xm
