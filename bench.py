@@ -177,6 +177,26 @@ def pmc_traffic(kernel, cfg):
     return int(c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024), d.get("source")
 
 
+def pmc_mfma_busy(kernel, cfg):
+    """Fraction of `kernel`'s duration its MFMA pipe is busy, from the committed
+    PMC summary's SQ_VALU_MFMA_BUSY_CYCLES (summed over the chip's 1024 SIMDs,
+    so / (1024 x 2.4 GHz) = busy us per SIMD) over the kernel-trace average of
+    the same summary; None when the summary is for another configuration."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("config") != cfg:
+        return None, None
+    c = d.get("counters", {}).get(kernel, {})
+    k = d.get("kernels", {}).get(kernel, {})
+    if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or not k.get("avg_us"):
+        return None, None
+    busy_us = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * 2.4e3)
+    return round(busy_us / k["avg_us"], 4), d.get("source")
+
+
 def spawn_ranks(n):
     """Re-launch this command under torchrun with n ranks (one per GPU) as a
     CHILD process -- nothing here has touched the GPU -- and return its status."""
@@ -379,6 +399,7 @@ def main():
     cfg_key = {"M": M, "N": N, "K": K, "Fin": Fin, "Fout": Fout}
     traffic, traffic_src = pmc_traffic(kern[dom]["kernel"].split("+")[0], cfg_key)
     fwd_traffic, _ = pmc_traffic(fwd_kernel, cfg_key)
+    mfma_busy, mfma_src = pmc_mfma_busy(fwd_kernel, cfg_key)
     contraction_tflops = 2.0 * N * M * Fin * K * Fout / (fwd_ms * 1e-3) / 1e12
     spmm_ach = bytes_fwd / (fwd_ms * 1e-3) / 1e9
 
@@ -431,7 +452,8 @@ def main():
                     for k, v in kern.items()},
         "contraction_mfma": {"tflops_over_fwd_kernel": round(contraction_tflops, 2),
                              "peak_tflops": MFMA_F32_PEAK_TF,
-                             "frac": round(contraction_tflops / MFMA_F32_PEAK_TF, 4)},
+                             "frac": round(contraction_tflops / MFMA_F32_PEAK_TF, 4),
+                             "busy_frac": mfma_busy, "busy_source": mfma_src},
         "compulsory_fwd_bytes": compulsory_fwd,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

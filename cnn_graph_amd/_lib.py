@@ -83,6 +83,10 @@ _SIGNATURES = {
     "cg_weight_grad": ([_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
     "cg_weight_grad_planes": ([_c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _vp, _c_i32, _vp, _c_sz,
                                _vp], _c_int),
+    "cg_lstm_weight_grads_workspace_bytes": ([_c_i64, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_sz)],
+                                            _c_int),
+    "cg_lstm_weight_grads": ([_c_i64, _c_i32, _c_i32, _c_i32, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp,
+                              _vp, _vp, _c_sz, _vp], _c_int),
     "cg_bias_grad_workspace_bytes": ([_c_i64, _c_i32, ctypes.POINTER(_c_sz)], _c_int),
     "cg_bias_grad": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _c_sz, _vp], _c_int),
     "cg_bias_act_forward": ([_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp], _c_int),
@@ -113,8 +117,8 @@ _SIGNATURES = {
     "cg_lstm_seq_forward_x": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp,
                                _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _c_sz,
                                _vp], _c_int),
-    "cg_lstm_bwd_step": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                          _vp, _vp, _vp, _vp], _c_int),
+    "cg_lstm_bwd_step": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp,
+                          _vp, _vp, _vp, _vp, _vp, _vp], _c_int),
     "cg_perm_gather": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),
     "cg_maxpool_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp], _c_int),
     "cg_maxpool_backward": ([_vp, _vp, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp], _c_int),

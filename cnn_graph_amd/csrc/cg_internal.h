@@ -284,9 +284,13 @@ hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, c
 int dw_chunks(int64_t R);
 // pl_fin > 0: basis in the planes layout (K planes of [R][pl_fin], pl_stride
 // floats apart); the slabs keep the rows layout's [Fin*K][Fout] order.
+// xb != NULL: x_fin*K more planes columns from xb (x_stride apart) and a
+// column of ones after the FinK basis columns (the gconv-LSTM's dWx and db in
+// the same pass over dy); the slabs are then [FinK + x_fin*K + 1][Fout].
 hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
                            float* slab, hipStream_t s, int pl_fin = 0, int64_t pl_stride = 0,
-                           int K = 0);
+                           int K = 0, const float* xb = nullptr, int x_fin = 0,
+                           int64_t x_stride = 0);
 // Number of K slices launch_gemm_f32 actually uses for `splits` requested.
 int gemm_effective_splits(int Kg, int splits);
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,
@@ -359,7 +363,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
                            int* status, int P, hipStream_t s);
 hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr, const int* tcol,
                              const float* tval, const int* order, int64_t nnzT, const float* dh, const float* dh_rec,
-                             const float* dc, const float* act, const float* c_prev,
+                             const float* dc, const float* act, int act_um, const float* c_prev,
                              const float* c_out, const float* Wh, float* dpre, float* dc_prev,
                              float* dh_prev, hipStream_t s);
 // Column sums of A [R][C] as [colsum_chunks(R)][C] partial slabs.

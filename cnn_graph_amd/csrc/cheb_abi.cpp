@@ -1228,6 +1228,50 @@ int cg_weight_grad_planes(int64_t R, int32_t Fin, int32_t K, int32_t Fout, const
   return ok();
 }
 
+static size_t lstm_wgrad_rows(int32_t H, int32_t Fin, int32_t K) {
+  return size_t(H + Fin) * size_t(K) + 1;
+}
+
+int cg_lstm_weight_grads_workspace_bytes(int64_t R, int32_t H, int32_t Fin, int32_t K,
+                                         size_t* bytes) {
+  if (!bytes || R < 1 || H < 1 || Fin < 1 || K < 1)
+    return fail(CG_ERR_ARG, "lstm_weight_grads: bad arguments");
+  const size_t rows = lstm_wgrad_rows(H, Fin, K);
+  *bytes = dw_slab_bytes(R, 0, int(rows), 4 * H) + al256(rows * size_t(4 * H) * 4);
+  return ok();
+}
+
+int cg_lstm_weight_grads(int64_t R, int32_t H, int32_t Fin, int32_t K, const float* h_planes,
+                         int64_t h_plane_stride, const float* x_planes, int64_t x_plane_stride,
+                         const float* dpre, float* dWh, float* dWx, float* db, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  if (!h_planes || !x_planes || !dpre || !dWh || !dWx || !db || R < 1 || H < 1 || Fin < 1 ||
+      K < 1 || h_plane_stride < R * H || x_plane_stride < R * Fin)
+    return fail(CG_ERR_ARG, "lstm_weight_grads: bad arguments");
+  if (4 * H > 256 || Fin * K + 1 > 64)
+    return fail(CG_ERR_UNSUPPORTED, "lstm_weight_grads: needs 4H <= 256, Fin*K < 64 (H=%d Fin=%d K=%d)",
+                H, Fin, K);
+  size_t need = 0;
+  int rc = cg_lstm_weight_grads_workspace_bytes(R, H, Fin, K, &need);
+  if (rc) return rc;
+  if (!workspace || ws_bytes < need)
+    return fail(CG_ERR_ARG, "lstm_weight_grads workspace too small: %zu < %zu", ws_bytes, need);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int rows = int(lstm_wgrad_rows(H, Fin, K)), C = 4 * H;
+  const size_t slab_bytes = dw_slab_bytes(R, 0, rows, C);
+  float* slabs = static_cast<float*>(workspace);
+  float* comb = reinterpret_cast<float*>(static_cast<char*>(workspace) + slab_bytes);
+  CG_HIP(cg::launch_dw_slabs(h_planes, dpre, R, H * K, C, slabs, s, H, h_plane_stride, K, x_planes,
+                             Fin, x_plane_stride));
+  CG_HIP(cg::launch_reduce_slabs(slabs, cg::dw_chunks(R), int64_t(rows) * C, comb, s));
+  CG_HIP(hipMemcpyAsync(dWh, comb, size_t(H) * K * C * 4, hipMemcpyDeviceToDevice, s));
+  CG_HIP(hipMemcpyAsync(dWx, comb + size_t(H) * K * C, size_t(Fin) * K * C * 4,
+                        hipMemcpyDeviceToDevice, s));
+  CG_HIP(hipMemcpyAsync(db, comb + size_t(H + Fin) * K * C, size_t(C) * 4, hipMemcpyDeviceToDevice,
+                        s));
+  return ok();
+}
+
 int cg_bias_grad_workspace_bytes(int64_t R, int32_t C, size_t* bytes) {
   if (!bytes || R < 1 || C < 1) return fail(CG_ERR_ARG, "bias_grad: bad arguments");
   *bytes = al256(size_t(cg::colsum_chunks(R)) * size_t(C) * 4);
@@ -1561,9 +1605,9 @@ int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, in
 }
 
 int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,
-                     const float* dh_rec, const float* dc, const float* act, const float* c_prev,
-                     const float* c_out, const float* Wh, float* dpre, float* dc_prev,
-                     float* dh_prev, void* stream) {
+                     const float* dh_rec, const float* dc, const float* act,
+                     int32_t act_unit_major, const float* c_prev, const float* c_out,
+                     const float* Wh, float* dpre, float* dc_prev, float* dh_prev, void* stream) {
   int rc = check_lstm(int64_t(N) * (plan ? plan->M : 1), H, gates);
   if (rc) return rc;
   if (!plan || N < 1 || K < 1) return fail(CG_ERR_ARG, "lstm_bwd_step: bad plan / N / K");
@@ -1583,7 +1627,7 @@ int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gat
   if ((rc = check_device(plan))) return rc;
   CG_HIP(cg::launch_lstm_bstep(gates, N, plan->M, K, plan->trowptr, plan->tcol, plan->tval,
                                plan->tlorder, plan->nnzT, dh, dh_rec,
-                               dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev,
+                               dc, act, act_unit_major, c_prev, c_out, Wh, dpre, dc_prev, dh_prev,
                                reinterpret_cast<hipStream_t>(stream)));
   return ok();
 }

@@ -565,6 +565,10 @@ __global__ __launch_bounds__(256) void k_gemm_f32(int Mg, int Ng, int Kg, const 
 // pl_fin > 0: the basis is in the planes layout (column jj = k*pl_fin + fin of
 // row r at basis[k*pl_stride + r*pl_fin + fin]); the slab keeps the rows
 // layout's column order fin*K + k.
+// xb != NULL (the gconv-LSTM weight gradients in one pass over dpre): FinKh
+// planes columns from `basis`, then x_fin*K planes columns from xb (plane
+// stride x_stride, slab column FinKh + fin*K + k) and one column of ones
+// (slab column FinK - 1: the bias gradient); FinK counts all of them.
 constexpr int kDwRB = 16;     // rows per LDS batch (4 per wave)
 constexpr int kDwTiles = 16;  // output tiles per block at most (4 per wave)
 constexpr int kDwNA = 2;      // basis pieces per lane and staged row (64 lanes x VW floats each)
@@ -576,7 +580,9 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
                                                   const float* __restrict__ dy, int64_t R,
                                                   int FinK, int Fout, int64_t rows_per_chunk,
                                                   float* __restrict__ slab, int pl_fin,
-                                                  int64_t pl_stride, int K, int tpb) {
+                                                  int64_t pl_stride, int K, int tpb,
+                                                  const float* __restrict__ xb, int x_fin,
+                                                  int64_t x_stride, int FinKh) {
   typedef typename std::conditional<VW == 4, float4, float>::type V;
   constexpr int kDwNB = dw_nb<VW>();
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -602,21 +608,29 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
   // dy columns VW*(lane + 64 i); their offsets from the row's base
   int64_t aoff[kDwNA];
   bool av[kDwNA], bv[kDwNB];
+  const int jhb = jhi < FinKh ? jhi : FinKh;  // the group's columns from `basis`
 #pragma unroll
   for (int i = 0; i < kDwNA; ++i) {
     const int cc = jlo + VW * (lane + 64 * i);
-    av[i] = cc < jhi;
+    av[i] = cc < jhb;
     aoff[i] = pl_fin > 0 ? int64_t(cc / pl_fin) * pl_stride + cc % pl_fin : cc;
   }
 #pragma unroll
   for (int i = 0; i < kDwNB; ++i) bv[i] = VW * (lane + 64 * i) < Fout;
-  const int64_t ald = pl_fin > 0 ? pl_fin : FinK;  // basis row stride
+  const int64_t ald = pl_fin > 0 ? pl_fin : FinKh;  // basis row stride
+  // the extra columns (xb): lane e stages column FinKh + e of each row
+  const int nxc = xb ? x_fin * K : 0;
+  const int xcol = FinKh + lane;
+  const bool xv = xb && lane <= nxc && xcol >= jlo && xcol < jhi;
+  const int64_t xoff = lane < nxc ? int64_t(lane / x_fin) * x_stride + lane % x_fin : 0;
   V ra[4][kDwNA], rbv[4][kDwNB];
+  float rx[4];
   auto fetch = [&](int64_t rb) {  // rows rb + 4w .. rb + 4w + 3 into registers
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int64_t rr = rb + 4 * w + q;
       const bool rv = rr < c1;
+      if (xv) rx[q] = lane == nxc ? 1.f : rv ? xb[xoff + rr * x_fin] : 0.f;
 #pragma unroll
       for (int i = 0; i < kDwNA; ++i)
         if (av[i]) ra[q][i] = rv ? *reinterpret_cast<const V*>(basis + rr * ald + aoff[i]) : V{};
@@ -630,6 +644,7 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
     for (int q = 0; q < 4; ++q) {
       float* da = s_a + (4 * w + q) * SA;
       float* db = s_b + (4 * w + q) * SB;
+      if (xv) da[xcol - jlo] = rx[q];
 #pragma unroll
       for (int i = 0; i < kDwNA; ++i)
         if (av[i]) {
@@ -680,7 +695,9 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jj = jt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const int jo = pl_fin > 0 ? (jj % pl_fin) * K + jj / pl_fin : jj;
+      const int jx = jj - FinKh;
+      const int jo = jj >= FinKh ? (jx < nxc ? FinKh + (jx % x_fin) * K + jx / x_fin : jj)
+                                 : pl_fin > 0 ? (jj % pl_fin) * K + jj / pl_fin : jj;
       if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jo) * Fout + ff] = acc[a][r];
     }
   }
@@ -873,13 +890,16 @@ int dw_chunks(int64_t R) {
   return int(c < 1 ? 1 : c);
 }
 
-hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
-                           float* slab, hipStream_t s, int pl_fin, int64_t pl_stride, int K) {
+hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
+                           float* slab, hipStream_t s, int pl_fin, int64_t pl_stride, int K,
+                           const float* xb, int x_fin, int64_t x_stride) {
   const int chunks = dw_chunks(R);
   const int64_t rpc = (R + chunks - 1) / chunks;
+  if (xb && (x_fin < 1 || x_fin * K + 1 > 64)) return hipErrorInvalidValue;
+  const int FinK = FinKh + (xb ? x_fin * K + 1 : 0);
   const int jtl = (FinK + 31) / 32, ftl = (Fout + 31) / 32;
   const int ntiles = jtl * ftl;
-  const int vw = (FinK % 4 == 0 && Fout % 4 == 0 && (pl_fin == 0 || pl_fin % 4 == 0)) ? 4 : 1;
+  const int vw = (FinKh % 4 == 0 && Fout % 4 == 0 && (pl_fin == 0 || pl_fin % 4 == 0)) ? 4 : 1;
   if (Fout > 256) return hipErrorInvalidValue;
   // tiles per block: as many as the staging pieces allow (every group
   // re-reads the chunk's dy rows and its own basis columns)
@@ -890,7 +910,7 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
     bool ok = true;
     for (int g = 0; g < groups; ++g) {
       const int t0 = g * tpb, t1 = std::min(t0 + tpb, ntiles);
-      const int jlo = (t0 / ftl) * 32, jhi0 = ((t1 - 1) / ftl + 1) * 32, jhi = std::min(jhi0, FinK);
+      const int jlo = (t0 / ftl) * 32, jhi0 = ((t1 - 1) / ftl + 1) * 32, jhi = std::min(jhi0, FinKh);
       span = std::max(span, jhi0 - jlo);
       if (jhi - jlo > kDwNA * 64 * vw) ok = false;
     }
@@ -901,10 +921,10 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
   const dim3 grid(chunks, groups);
   if (vw == 4)
     hipLaunchKernelGGL(k_dw_slabs<4>, grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
-                       slab, pl_fin, pl_stride, K, tpb);
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
   else
     hipLaunchKernelGGL(k_dw_slabs<1>, grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
-                       slab, pl_fin, pl_stride, K, tpb);
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
   return hipGetLastError();
 }
 

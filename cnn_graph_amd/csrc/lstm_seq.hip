@@ -136,7 +136,7 @@ struct SeqArgs {
   const float* c0;    // [N][M][32] or NULL
   float* hs;          // [T][N][M][32]
   float* cs;          // [T][N][M][32]
-  float* act;         // [T][N][M][128] gate activations, or NULL
+  float* act;         // [T][N][M][32][4] gate activations z|i|f|o per unit (unit-major), or NULL
   float* planes;      // T_k of h_{t-1} at (k-1)*pstride + [T][N][M][32], or NULL
   int64_t pstride;
   int* flags;         // [P][2] step counters (zeroed before the launch)
@@ -182,10 +182,11 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
     s_W[e] = A.Wh[int64_t(ch * K + k) * 128 + gcol];
   }
   if (A.xs) {
-    // x channel c = 4hh + s of MFMA step s (zero past Fin)
+    // x channel c = 2s + hh of MFMA step s (zero past Fin): Fin <= 2 needs
+    // one step per order, not four
     for (int e = tid; e < K * 512; e += kST) {
       const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3, k = e >> 9;
-      const int c = 4 * h2 + s;
+      const int c = 2 * s + h2;
       const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
       s_Wx[e] = c < A.Fin ? A.Wx[int64_t(c * K + k) * 128 + gcol] : 0.f;
     }
@@ -240,14 +241,30 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
       const __amdgpu_buffer_rsrc_t r_hout = slab_rsrc(A.hs + (int64_t(t) * N + n) * M * kH, M);
       // gates^T += Wh_k^T T_k^T over quarter q's 8 channels; B operand: the
       // lane's own rows of T_k (tk, channels 8q + 4hh .. +3)
-      auto contract = [&](int q, int k, const float4* tk) {  // q = 4: the x quarter
-        const float* wq = (q < 4 ? s_W + (k * 4 + q) * 512 : s_Wx + k * 512) + hh * 64 + j;
+      auto contract = [&](int q, int k, const float4* tk) {
+        const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
 #pragma unroll
         for (int s = 0; s < 4 && !CG_DBG(A.dbg, 1); ++s) {
           const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
 #pragma unroll
           for (int rt = 0; rt < kRT; ++rt) {
             const float b = (&tk[rt].x)[s];
+            acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[rt][0], 0, 0, 0);
+            acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[rt][1], 0, 0, 0);
+          }
+        }
+      };
+      // the x quarter's contraction: MFMA step s takes channel 2s + hh of the
+      // lane's rows straight from the LDS slot, steps past Fin skipped
+      auto contract_x = [&](int k, const float* cur) {
+        const float* wq = s_Wx + k * 512 + hh * 64 + j;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (2 * s >= A.Fin || CG_DBG(A.dbg, 1)) break;
+          const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
+#pragma unroll
+          for (int rt = 0; rt < kRT; ++rt) {
+            const float b = cur[row[rt] * kQ + 2 * s + hh];
             acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[rt][0], 0, 0, 0);
             acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[rt][1], 0, 0, 0);
           }
@@ -275,11 +292,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
         __syncthreads();
         for (int k = 0; k < K; ++k) {
           const float* cur = (k & 1) ? slot1 : slot0;
-          float4 tk[kRT];
-#pragma unroll
-          for (int rt = 0; rt < kRT; ++rt)
-            tk[rt] = *reinterpret_cast<const float4*>(cur + row[rt] * kQ + 4 * hh);
-          contract(4, k, tk);
+          contract_x(k, cur);
           if (k + 1 < K) {
             float* nxt = (k & 1) ? slot0 : slot1;
 #pragma unroll
@@ -475,11 +488,12 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           if (!CG_DBG(A.dbg, 256))
             bst16_sc1(r_hout, row[rt] * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
           if (A.act && !CG_DBG(A.dbg, 64)) {
-            float* ap = A.act + rr * 128 + u0;
-            *reinterpret_cast<float4*>(ap) = make_float4(zz[0], zz[1], zz[2], zz[3]);
-            *reinterpret_cast<float4*>(ap + 32) = make_float4(ii[0], ii[1], ii[2], ii[3]);
-            *reinterpret_cast<float4*>(ap + 64) = make_float4(ff[0], ff[1], ff[2], ff[3]);
-            *reinterpret_cast<float4*>(ap + 96) = make_float4(oo[0], oo[1], oo[2], oo[3]);
+            // unit-major: the 4 gates of a unit side by side, the lane's 4
+            // units one contiguous 64-byte record
+            float* ap = A.act + rr * 128 + 4 * u0;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+              *reinterpret_cast<float4*>(ap + 4 * m) = make_float4(zz[m], ii[m], ff[m], oo[m]);
           }
         }
       }
@@ -493,11 +507,11 @@ struct BStepArgs {
   const int* tcol;
   const float* tval;
   const int* order;    // rows of L~^T by decreasing length (lane -> row)
-  int M, Mr, N, gates, pair_xcd, nnz;
+  int M, Mr, N, gates, pair_xcd, nnz, act_um;
   const float* dh;      // [N][M][32] gradient of h' from above, or NULL
   const float* dh_rec;  // [N][M][32] gradient of h' from step t+1's h-conv, or NULL
   const float* dc;      // [N][M][32] gradient of c', or NULL
-  const float* act;     // [N][M][128]
+  const float* act;     // [N][M][128]: [g][32] (gate-major) or [32][g] (unit-major, act_um)
   const float* c_prev;  // [N][M][32] or NULL (zero state)
   const float* c_out;   // [N][M][32]
   const float* Wh;      // [K*32][128]
@@ -563,15 +577,24 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     float dp[4][8];
     if (row < M) {
       const int64_t rr = int64_t(n) * M + row;
-      const float* ap = A.act + rr * 128 + 8 * q;
       const int64_t hb = rr * kH + 8 * q;
       float av[4][8], cp[8], co[8], dhv[8], dcv[8];
+      if (A.act_um) {  // units 8q .. 8q+7: one contiguous 128-byte record
+        const float* ap = A.act + rr * 128 + 32 * q;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 x0 = *reinterpret_cast<const float4*>(ap + g * 32);
-        const float4 x1 = *reinterpret_cast<const float4*>(ap + g * 32 + 4);
-        av[g][0] = x0.x; av[g][1] = x0.y; av[g][2] = x0.z; av[g][3] = x0.w;
-        av[g][4] = x1.x; av[g][5] = x1.y; av[g][6] = x1.z; av[g][7] = x1.w;
+        for (int m = 0; m < 8; ++m) {
+          const float4 x = *reinterpret_cast<const float4*>(ap + 4 * m);
+          av[0][m] = x.x; av[1][m] = x.y; av[2][m] = x.z; av[3][m] = x.w;
+        }
+      } else {
+        const float* ap = A.act + rr * 128 + 8 * q;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 x0 = *reinterpret_cast<const float4*>(ap + g * 32);
+          const float4 x1 = *reinterpret_cast<const float4*>(ap + g * 32 + 4);
+          av[g][0] = x0.x; av[g][1] = x0.y; av[g][2] = x0.z; av[g][3] = x0.w;
+          av[g][4] = x1.x; av[g][5] = x1.y; av[g][6] = x1.z; av[g][7] = x1.w;
+        }
       }
       auto ld8 = [&](const float* base, float* out) {
         if (base) {
@@ -780,12 +803,12 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
 
 hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr, const int* tcol,
                              const float* tval, const int* order, int64_t nnzT, const float* dh, const float* dh_rec,
-                             const float* dc, const float* act, const float* c_prev,
+                             const float* dc, const float* act, int act_um, const float* c_prev,
                              const float* c_out, const float* Wh, float* dpre, float* dc_prev,
                              float* dh_prev, hipStream_t s) {
   if (!lstm_bstep_ok(M, kH, K, nnzT) || N < 1) return hipErrorInvalidValue;
   BStepArgs a{trowptr, tcol, tval, order, M, round_up(M + 1, 16), N, gates, N % 8 == 0 ? 1 : 0,
-              int(nnzT), dh, dh_rec, dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev};
+              int(nnzT), act_um ? 1 : 0, dh, dh_rec, dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev};
   const size_t lds = lstm_bstep_lds(M, K, nnzT);
 #define CG_BSTEP(KK)                                                                              \
   case KK: {                                                                                      \

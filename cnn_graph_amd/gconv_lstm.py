@@ -245,7 +245,7 @@ class _Layer(torch.autograd.Function):
             gx = gx.view(T, R, 4 * H)
         hs = torch.empty((T, N, M, H), **f32)
         cs = torch.empty((T, N, M, H), **f32)
-        act = torch.empty((T, R, 4 * H), **f32)
+        act = torch.empty((T, R, 4 * H), **f32)  # unit-major [R][H][4] on the seq path
         fused = cell.fused or cell.seq
         # h bases kept for the backward's weight gradient: the fused h-step
         # writes the orders 1..K-1 as planes [K-1][T][R][H] (order 0 is h_prev)
@@ -261,6 +261,8 @@ class _Layer(torch.autograd.Function):
             hp = torch.empty((K, T + 1, R, H), **f32)
             if not zero_init:
                 hp[0, 0].copy_(h0.reshape(R, H))
+            elif seq_x:  # no h-conv at step 0: zero rows for the one-pass weight gradients
+                hp[:, 0].zero_()
             hs = hp[0, 1:].view(T, N, M, H)
             planes = hp
             if seq_x:
@@ -310,9 +312,12 @@ class _Layer(torch.autograd.Function):
                 # reverse recurrence over L~^T -> the gradient of h_{t-1}
                 _, dc, dh_rec = ops.lstm_bwd_step(plan, None if dhs is None else dhs[t], dh_rec,
                                                   dc, act[t], c_prev, cs[t], Wh, K, gates,
-                                                  out_dpre=dpre[t])
+                                                  out_dpre=dpre[t], act_unit_major=True)
                 continue
-            dpre_t, dc = ops.lstm_cell_backward(None if dhs is None else dhs[t], dh_rec, dc, act[t],
+            # the sequence kernel's act records are unit-major: gate-major for the
+            # pointwise kernel (step 0 of a zero-state layer only)
+            act_t = act[t].view(R, H, 4).transpose(1, 2).reshape(R, 4 * H) if cell.seq else act[t]
+            dpre_t, dc = ops.lstm_cell_backward(None if dhs is None else dhs[t], dh_rec, dc, act_t,
                                                 c_prev, cs[t], H, gates, out_dpre=dpre[t])
             if t >= t_first:
                 dh_rec, _ = ops.cheb_backward(plan, dpre[t].view(N, M, 4 * H),
@@ -320,6 +325,19 @@ class _Layer(torch.autograd.Function):
                                               need_dW=False)
             else:
                 dh_rec = None
+        if ctx.seq_x:
+            # dWh, dWx and db in ONE pass over dpre: the h planes of every step
+            # (a zero-state layer's step 0 has none: the forward zeroed its slots) and
+            # the x planes [K][T*R][F] (dx needs no basis)
+            dWh, dWx, db = ops.lstm_weight_grads(hb[0, 0:T].reshape(-1, H), (T + 1) * R * H,
+                                                 basis_x[0], T * R * F, K, T * R, dpre)
+            dxs = None
+            if ctx.needs_input_grad[0]:
+                dxs, _ = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), None, Wx, K,
+                                           need_dW=False)
+            dx_out = dxs.view(T, N, M, F) if dxs is not None else None
+            return (dx_out, None if zero_init else dc, None if zero_init else dh_rec, dWx, dWh, db,
+                    None, None)
         if T <= t_first:
             dWh = torch.zeros_like(Wh)
         elif cell.seq:  # one GEMM over the K planes of every step with an h-conv
@@ -337,15 +355,8 @@ class _Layer(torch.autograd.Function):
                                        H, K)
         else:
             dWh = ops.weight_grad(hb[t_first:], dpre[t_first:])
-        if ctx.seq_x:  # the x basis as K planes [T*R][F]: one planes GEMM; dx needs no basis
-            dWx = ops.weight_grad_planes(basis_x[0], T * R * F, K, T * R, dpre)
-            dxs = None
-            if ctx.needs_input_grad[0]:
-                dxs, _ = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), None, Wx, K,
-                                           need_dW=False)
-        else:
-            dxs, dWx = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), basis_x, Wx, K,
-                                         need_dx=ctx.needs_input_grad[0])
+        dxs, dWx = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), basis_x, Wx, K,
+                                     need_dx=ctx.needs_input_grad[0])
         db = ops.bias_grad(dpre)
         dx_out = dxs.view(T, N, M, F) if dxs is not None else None
         dc0 = None if zero_init else dc

@@ -489,6 +489,35 @@ def weight_grad_planes(planes: torch.Tensor, plane_stride: int, K: int, R: int, 
     return out
 
 
+def lstm_weight_grads(h_planes: torch.Tensor, h_plane_stride: int, x_planes: torch.Tensor,
+                      x_plane_stride: int, K: int, R: int, dpre: torch.Tensor):
+    """dWh [H*K, 4H], dWx [Fin*K, 4H] and db [4H] of a gconv-LSTM layer in ONE
+    pass over dpre [R, 4H] (cg_lstm_weight_grads): the K h planes [R, H] of
+    h_planes' storage h_plane_stride floats apart, the K x planes [R, Fin] of
+    x_planes' storage likewise."""
+    for name, t in (("h_planes", h_planes), ("x_planes", x_planes), ("dpre", dpre)):
+        _check_dev(name, t)
+    H, Fin = int(h_planes.shape[-1]), int(x_planes.shape[-1])
+    if dpre.numel() != R * 4 * H or not dpre.is_contiguous():
+        raise ValueError(f"dpre must be a contiguous tensor of R*4H = {R * 4 * H} elements")
+    for name, t, st, w in (("h_planes", h_planes, h_plane_stride, H),
+                           ("x_planes", x_planes, x_plane_stride, Fin)):
+        avail = t.untyped_storage().nbytes() // 4 - t.storage_offset()
+        if st < R * w or avail < (K - 1) * st + R * w:
+            raise ValueError(f"{name}: storage too small for K planes at this stride")
+    f32 = dict(device=dpre.device, dtype=torch.float32)
+    dWh = torch.empty((H * K, 4 * H), **f32)
+    dWx = torch.empty((Fin * K, 4 * H), **f32)
+    db = torch.empty((4 * H,), **f32)
+    nb = ctypes.c_size_t()
+    _lib.call("cg_lstm_weight_grads_workspace_bytes", int(R), H, Fin, int(K), ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 1), device=dpre.device, dtype=torch.uint8)
+    _lib.call("cg_lstm_weight_grads", int(R), H, Fin, int(K), _p(h_planes), int(h_plane_stride),
+              _p(x_planes), int(x_plane_stride), _p(dpre), _p(dWh), _p(dWx), _p(db), _p(ws),
+              nb.value, _stream(dpre))
+    return dWh, dWx, db
+
+
 def bias_grad(dy: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False):
     """db = dy summed over every axis but the last (gradient of a broadcast bias)."""
     _check_dev("dy", dy)
@@ -623,7 +652,9 @@ def lstm_seq_forward(plan: ChebPlan, gx, Wh, bias, K: int, T: int, N: int, gates
     (zero state).  planes (optional; a tensor whose storage holds K-1 planes
     [T, N, M, H] plane_stride floats apart) receives T_k of h_{t-1}, k >= 1.
     check=True waits for the stream and raises if a pair hand-off timed out.
-    Returns (hs [T, N, M, H], cs [T, N, M, H], act [T, N, M, 4H] or None)."""
+    Returns (hs [T, N, M, H], cs [T, N, M, H], act or None) -- act UNIT-major,
+    [T, N, M, 4H] holding act[..., 4u + g] (g = z, i, f, o): lstm_bwd_step
+    reads it with act_unit_major=True."""
     _check_dev("gx", gx)
     H = int(Wh.shape[1]) // 4
     M = plan.M
@@ -723,10 +754,13 @@ def lstm_seq_forward_x(plan: ChebPlan, xs, Wx, Wh, bias, K: int, gates="referenc
 
 
 def lstm_bwd_step(plan: ChebPlan, dh, dh_rec, dc, act, c_prev, c_out, Wh, K: int,
-                  gates="reference", out_dpre=None, need_dc_prev=True, out_dh_prev=None):
+                  gates="reference", out_dpre=None, need_dc_prev=True, out_dh_prev=None,
+                  act_unit_major=False):
     """One BPTT step of a gconv-LSTM layer in ONE launch (cg_lstm_bwd_step):
     dpre = the gradient of the gate pre-activations, dc_prev, and dh_prev =
     the h-conv's input gradient.  dh / dh_rec / dc / c_prev may be None (= 0).
+    act: gate-major [..., 4H] (lstm_cell_forward / lstm_hconv_step) or, with
+    act_unit_major, the unit-major [..., H, 4] records of lstm_seq_forward*.
     Returns (dpre [..., 4H], dc_prev [..., H] or None, dh_prev [..., H])."""
     _check_dev("act", act)
     _check_dev("c_out", c_out)
@@ -745,13 +779,15 @@ def lstm_bwd_step(plan: ChebPlan, dh, dh_rec, dc, act, c_prev, c_out, Wh, K: int
     if tuple(Wh.shape) != (K * H, 4 * H) or not Wh.is_contiguous():
         raise ValueError(f"Wh must be a contiguous [{K * H}, {4 * H}] tensor")
     f32 = dict(device=dev, dtype=torch.float32)
-    dpre = out_dpre if out_dpre is not None else torch.empty(tuple(act.shape), **f32)
+    dpre = out_dpre if out_dpre is not None else \
+        torch.empty(tuple(c_out.shape[:-1]) + (4 * H,), **f32)
     _check_out("dpre", dpre, (R, 4 * H))
     dc_prev = torch.empty(tuple(c_out.shape), **f32) if need_dc_prev else None
     dh_prev = out_dh_prev if out_dh_prev is not None else torch.empty(tuple(c_out.shape), **f32)
     _check_out("dh_prev", dh_prev, (R, H))
     _lib.call("cg_lstm_bwd_step", plan.handle, int(N), int(H), int(K), LSTM_GATES[gates], _p(dh),
-              _p(dh_rec), _p(dc), _p(act), _p(c_prev), _p(c_out), _p(Wh), _p(dpre), _p(dc_prev),
+              _p(dh_rec), _p(dc), _p(act), int(bool(act_unit_major)), _p(c_prev), _p(c_out), _p(Wh),
+              _p(dpre), _p(dc_prev),
               _p(dh_prev), _stream(act))
     return dpre, dc_prev, dh_prev
 

@@ -232,6 +232,21 @@ int cg_weight_grad(int64_t R, int32_t FinK, int32_t Fout, const float* basis, co
 int cg_weight_grad_planes(int64_t R, int32_t Fin, int32_t K, int32_t Fout, const float* planes,
                           int64_t plane_stride, const float* dy, float* dW, int32_t accumulate,
                           void* workspace, size_t ws_bytes, void* stream);
+/* The three weight gradients of a gconv-LSTM layer in ONE pass over dpre
+ * [R][4H] (lib/gconv_lstm.py:183-207's two cheby_conv weights and the gate
+ * bias, summed over every step of the layer; R = T*N*M):
+ *   dWh [H*K][4H] (row c*K + k) = sum_k T_k(h)^T dpre, h planes: K planes
+ *       [R][H] h_plane_stride floats apart (rows of a step without an h-conv
+ *       must hold zeros);
+ *   dWx [Fin*K][4H] (row f*K + k) from the x planes [R][Fin] likewise;
+ *   db [4H] = column sums of dpre.
+ * Fixed-order reduction (bitwise reproducible).  4H <= 256, Fin*K < 64. */
+int cg_lstm_weight_grads_workspace_bytes(int64_t R, int32_t H, int32_t Fin, int32_t K,
+                                         size_t* bytes);
+int cg_lstm_weight_grads(int64_t R, int32_t H, int32_t Fin, int32_t K, const float* h_planes,
+                         int64_t h_plane_stride, const float* x_planes, int64_t x_plane_stride,
+                         const float* dpre, float* dWh, float* dWx, float* db, void* workspace,
+                         size_t ws_bytes, void* stream);
 /* db[c] (+)= sum_r dy[r][c] -- gradient of a broadcast bias add, dy [R][C]. */
 int cg_bias_grad_workspace_bytes(int64_t R, int32_t C, size_t* bytes);
 int cg_bias_grad(int64_t R, int32_t C, const float* dy, float* db, int32_t accumulate,
@@ -331,8 +346,10 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
  * per-step flag; c kept in registers; L~ and Wh staged in LDS once).
  *   gx [T][N][M][4H]  the x-conv of every step (chebyshev5 of the [T*N] batch)
  *   h0, c0 [N][M][H]  initial state, NULL = zero state (step 0 then has no h-conv)
- *   hs, cs [T][N][M][H] OUT: h_t and c_t;  act [T][N][M][4H] OUT (nullable):
- *   gate activations z|i|f|o;  planes (required for K > 1): T_k of h_{t-1} for
+ *   hs, cs [T][N][M][H] OUT: h_t and c_t;  act [T][N][M][H][4] OUT (nullable):
+ *   gate activations UNIT-major, act[r][4u + g] with g = z|i|f|o (each lane's
+ *   4 units leave as one 64-byte record; cg_lstm_bwd_step reads it with
+ *   act_unit_major = 1);  planes (required for K > 1): T_k of h_{t-1} for
  *   k = 1..K-1 at (k-1)*plane_stride + [T][N][M][H] (steps with an h-conv
  *   only; each workgroup computes the orders of its own 16 channels and reads
  *   its partner's from here)
@@ -343,6 +360,8 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
  *   gate pre-activations, [N][M][4H]), dc_prev and dh_prev = the h-conv's
  *   input gradient (reverse Chebyshev recurrence over L~^T of dpre Wh^T).
  *   dh / dh_rec / dc / c_prev nullable (= 0), dc_prev nullable.  K <= 4.
+ *   act_unit_major: 0 = act [N][M][4H] gate-major (cg_lstm_cell_forward /
+ *   cg_lstm_hconv_step), 1 = unit-major [N][M][H][4] (cg_lstm_seq_forward*).
  * ------------------------------------------------------------------------- */
 int cg_lstm_seq_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* supported);
 int cg_lstm_seq_workspace_bytes(const cg_plan* plan, int32_t N, size_t* bytes);
@@ -364,9 +383,9 @@ int cg_lstm_seq_forward_x(cg_plan* plan, int32_t T, int32_t N, int32_t Fin, int3
 int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,
                        void* stream);
 int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,
-                     const float* dh_rec, const float* dc, const float* act, const float* c_prev,
-                     const float* c_out, const float* Wh, float* dpre, float* dc_prev,
-                     float* dh_prev, void* stream);
+                     const float* dh_rec, const float* dc, const float* act,
+                     int32_t act_unit_major, const float* c_prev, const float* c_out,
+                     const float* Wh, float* dpre, float* dc_prev, float* dh_prev, void* stream);
 
 /* ---------------------------------------------------------------------------
  * perm_data (lib/coarsening.py:219-240) on device:

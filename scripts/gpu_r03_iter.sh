@@ -11,3 +11,9 @@ grep -E "FAIL|Error|passed|failed" $O/pytest.txt | tail -20
 [ $rc -eq 0 ] || { echo PYTEST_FAIL; exit 1; }
 timeout -k 10 300 python3 scripts/ablate_lstm.py > $O/ablate_lstm.json 2> $O/ablate_lstm.err && cat $O/ablate_lstm.json &&
 timeout -k 10 300 python3 scripts/bench_configs.py E R > $O/configs.jsonl 2> $O/configs.err && cat $O/configs.jsonl
+[ -n "$KT" ] || exit 0
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ktE -o kt --output-format csv -- python3 scripts/bench_configs.py E > $O/ktE.log 2>&1 && echo KTE_OK &&
+python3 scripts/pmc_table.py $O/ktE > $O/tableE.json && head -c 2500 $O/tableE.json
+[ -n "$KTR" ] || exit 0
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ktR -o kt --output-format csv -- python3 scripts/bench_configs.py R > $O/ktR.log 2>&1 && echo KTR_OK &&
+python3 scripts/pmc_table.py $O/ktR > $O/tableR.json

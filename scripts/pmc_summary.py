@@ -50,6 +50,11 @@ def main(root, tag=None):
             c["FETCH_SIZE_x2_bytes"] = c["FETCH_SIZE"] * 1024 * 2
         if "WRITE_SIZE" in c:
             c["WRITE_SIZE_bytes"] = c["WRITE_SIZE"] * 1024
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+            # summed over the 1024 SIMDs, shader clock 2.4 GHz: busy us of one SIMD
+            c["mfma_busy_us"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * 2.4e3), 3)
+            if k in out["kernels"]:
+                c["mfma_busy_frac"] = round(c["mfma_busy_us"] / out["kernels"][k]["avg_us"], 4)
     print(json.dumps(out, indent=1))
 
 

@@ -296,6 +296,11 @@ def test_bwd_step_equals_pointwise_plus_cheb_backward(dev, K, gates):
             assert torch.equal(dpre, rdpre)
             assert torch.equal(dcp, rdcp)
             assert O.normwise_err(dhp.cpu().numpy(), rdhp.cpu().numpy().astype(np.float64)) < 1e-6
+            # the unit-major act records of the sequence kernel: the same step
+            act_um = act.view(N, M, 4, H).transpose(-1, -2).contiguous()
+            d2, c2, h2 = ops.lstm_bwd_step(plan, a_dh, a_dhr, a_dc, act_um, a_cp, c_out, Wh, K, gates,
+                                           act_unit_major=True)
+            assert torch.equal(d2, dpre) and torch.equal(c2, dcp) and torch.equal(h2, dhp)
 
 
 def test_seq_forward_more_samples_than_pairs(dev):
@@ -367,3 +372,35 @@ def test_config_E_full_batch_gradients_vs_oracle(dev):
         assert err < TOL, (name, err)
     rest = [i for i in range(N) if i not in sel]
     assert int(torch.count_nonzero(xa.grad[:, rest])) == 0
+
+
+@pytest.mark.parametrize("Fin,K", [(2, 3), (1, 1), (8, 4), (5, 2)])
+def test_lstm_weight_grads_one_pass(dev, Fin, K):
+    """cg_lstm_weight_grads (dWh, dWx and db of a layer in one pass over dpre)
+    against the per-weight kernels: dWh and dWx bitwise equal to
+    cg_weight_grad_planes (same chunks, same per-tile row order), db within
+    1e-6 of cg_bias_grad (ones column on the MFMA vs a column-sum kernel), and
+    all three against float64."""
+    from cnn_graph_amd import ops
+    H, R = 32, 3 * 1021
+    g = torch.Generator(device=dev)
+    g.manual_seed(7 * Fin + K)
+    hst, xst = R * H + 96, R * Fin + 40
+    hbuf = torch.randn((K * hst,), device=dev, generator=g)
+    xbuf = torch.randn((K * xst,), device=dev, generator=g)
+    dpre = torch.randn((R, 4 * H), device=dev, generator=g)
+    hpl, xpl = hbuf[:R * H].view(R, H), xbuf[:R * Fin].view(R, Fin)
+    dWh, dWx, db = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
+    rWh = ops.weight_grad_planes(hpl, hst, K, R, dpre)
+    rWx = ops.weight_grad_planes(xpl, xst, K, R, dpre)
+    rdb = ops.bias_grad(dpre)
+    torch.cuda.synchronize()
+    assert torch.equal(dWh, rWh)
+    assert torch.equal(dWx, rWx)
+    assert O.normwise_err(db.cpu().numpy(), rdb.cpu().numpy().astype(np.float64)) < 1e-6
+    d64 = dpre.double().cpu()
+    for buf, st, w, got in ((hbuf, hst, H, dWh), (xbuf, xst, Fin, dWx)):
+        pl = torch.stack([buf[k * st:k * st + R * w].view(R, w) for k in range(K)]).double().cpu()
+        ref = torch.einsum("krc,rg->ckg", pl, d64).reshape(w * K, 4 * H)
+        assert O.normwise_err(got.cpu().numpy(), ref.numpy()) < 1e-5
+    assert O.normwise_err(db.cpu().numpy(), d64.sum(0).numpy()) < 1e-5
