@@ -14,6 +14,7 @@
 //             v_mfma_f32_32x32x2_f32, transposed (y^T = W^T T^T) so the B
 //             operand is the lane's own T_k straight from the SpMM; the
 //             per-group partial y_g leaves once per filter.
+// k_grp16_fwd the same with 16-channel groups and one LDS slot (Fin % 16 == 0).
 // k_grp_yred  y = act(sum_g y_g + res), groups added in a fixed order.
 // k_grp_clen  the backward's reverse recurrence G_{K-1} = D_{K-1},
 //             G_k = (D_k + c L~^T G_{k+1}) - G_{k+2} (c = 2; 1 at k = 0) over the
@@ -40,6 +41,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kGT = 512;  // threads per workgroup
 constexpr int kGQ = 8;    // channels per group
 constexpr int kGRT = 4;   // 32-row tiles per wave (8 waves x 4 x 32 = 1024 rows)
+constexpr int kGQ16 = 16; // channels per group of the one-slot kernels (Fin % 16 == 0)
 
 inline int rup(int v, int m) { return (v + m - 1) / m * m; }
 
@@ -168,6 +170,160 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
         *own = o;
         *reinterpret_cast<float4*>(pl + (int64_t(n) * M + rowS[rt]) * Fin + c0) = o;
       }
+      __syncthreads();
+    }
+  }
+  if (!want_y) return;
+  // lane (row, hh) holds outputs ot*32 + 8q + 4hh + m (q = e / 4, m = e % 4)
+  float* yg = A.yp + int64_t(g) * A.N * M * Fout;
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    if (row[rt] >= M) continue;
+    float* yr = yg + (int64_t(n) * M + row[rt]) * Fout;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int o0 = ot * 32 + 8 * q + 4 * hh;
+        if (o0 + 4 <= Fout && (Fout & 3) == 0) {
+          *reinterpret_cast<float4*>(yr + o0) =
+              make_float4(acc[rt][ot][4 * q], acc[rt][ot][4 * q + 1], acc[rt][ot][4 * q + 2],
+                          acc[rt][ot][4 * q + 3]);
+        } else {
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            if (o0 + m < Fout) yr[o0 + m] = acc[rt][ot][4 * q + m];
+        }
+      }
+  }
+}
+
+// The same forward for 16-channel groups (Fin % 16 == 0): half the workgroups
+// of the 8-channel kernel, so config R's 100 samples x 2 groups fit the 256
+// CUs in ONE round (8-channel groups: 416 workgroups = two rounds, the second
+// 62 % full); measured 178 vs 192 us per call (profiles/r03_grp): a workgroup
+// with twice the channels takes nearly twice as long, the chip is busy either way.  ONE [M][16] slot: a step gathers T_k from it, each lane keeps
+// T_{k-1} of its own rows in registers, a barrier, the lane swaps its rows'
+// T_k out for T_{k+1}, a barrier.  SpMM lanes: (row lane / 4 of a 16-row half
+// tile, channels 4 (lane % 4) ..); MFMA lanes: (row j, channels 8hh .. 8hh+7).
+// Fout <= 32 only (NOT = 1; two output tiles spill at 256 registers).
+template <int NOT>
+__global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  int n, g;
+  grp_map(blockIdx.x, A.G, n, g);
+  if (n >= A.N) return;  // grid padded to whole XCD rounds (uniform per workgroup)
+  const int M = A.M, K = A.K, Fin = A.Fin, Fout = A.Fout;
+  float* slot = smem;                     // [Mr][16]
+  float* s_W = slot + A.Mr * kGQ16;       // [K][s 8][hh 2][NOT][i 32]
+  float* s_val = s_W + K * 512 * NOT;
+  unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
+  const bool want_y = A.yp != nullptr;
+  if (want_y) {
+    for (int e = tid; e < K * 512 * NOT; e += kGT) {
+      const int i = e & 31, ot = (e >> 5) % NOT, h2 = (e / (32 * NOT)) & 1;
+      const int s = (e / (64 * NOT)) & 7, k = e / (512 * NOT);
+      const int ch = kGQ16 * g + 8 * h2 + s, out = ot * 32 + i;
+      s_W[e] = out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
+    }
+  }
+  for (int e = tid; e < A.nnz; e += kGT) {
+    s_val[e] = A.val[e];
+    s_col[e] = static_cast<unsigned short>(A.col[e]);
+  }
+  if (tid < kGQ16) slot[M * kGQ16 + tid] = 0.f;  // zero row M
+  const int js = lane >> 2, qs = lane & 3;
+  const int c0 = kGQ16 * g + 4 * qs;
+  // per (tile, half): the row, its CSR start | length << 16 (nnz < 65536 and
+  // rows <= 1024 long: the LDS bound), the wave's longest row (uniform)
+  int row[kGRT], rowS[kGRT][2], rbl[kGRT][2], wl[kGRT][2];
+  bool rvS[kGRT][2];
+  float4 tm1[kGRT][2];
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    const int idx = (wave + 8 * rt) * 32 + j;
+    row[rt] = idx < M ? A.order[idx] : M;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int idxS = (wave + 8 * rt) * 32 + 16 * hf + js;
+      rvS[rt][hf] = idxS < M;
+      rowS[rt][hf] = rvS[rt][hf] ? A.order[idxS] : M;
+      const int b0 = rvS[rt][hf] ? A.rowptr[rowS[rt][hf]] : 0;
+      const int len = rvS[rt][hf] ? A.rowptr[rowS[rt][hf] + 1] - b0 : 0;
+      rbl[rt][hf] = b0 | (len << 16);
+      wl[rt][hf] = __builtin_amdgcn_readfirstlane(wave_max(len));
+      tm1[rt][hf] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (rvS[rt][hf]) {
+        const int64_t o = (int64_t(n) * M + rowS[rt][hf]) * Fin + c0;
+        const float4 v = *reinterpret_cast<const float4*>(A.x + o);
+        *reinterpret_cast<float4*>(A.basis + o) = v;  // plane 0 = x
+        *reinterpret_cast<float4*>(slot + rowS[rt][hf] * kGQ16 + 4 * qs) = v;
+      }
+    }
+  }
+  f32x16 acc[kGRT][NOT];
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[rt][ot][e] = 0.f;
+  __syncthreads();
+  for (int k = 0; k < K; ++k) {
+    if (want_y) {
+      // y^T[out][row] += W_k^T[out][ch] T_k^T[ch][row], channels 8hh + s
+      const float* wk = s_W + k * 512 * NOT + hh * 32 * NOT + j;
+      float4 ta[kGRT], tb[kGRT];
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt) {
+        ta[rt] = *reinterpret_cast<const float4*>(slot + row[rt] * kGQ16 + 8 * hh);
+        tb[rt] = *reinterpret_cast<const float4*>(slot + row[rt] * kGQ16 + 8 * hh + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) {
+          const float a = wk[s * 64 * NOT + ot * 32];
+#pragma unroll
+          for (int rt = 0; rt < kGRT; ++rt) {
+            const float b = s < 4 ? (&ta[rt].x)[s] : (&tb[rt].x)[s - 4];
+            acc[rt][ot] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[rt][ot], 0, 0, 0);
+          }
+        }
+    }
+    if (k + 1 < K) {
+      float4 nv[kGRT][2];
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          if (!rvS[rt][hf]) continue;
+          float4 sm;
+          const int b0 = rbl[rt][hf] & 0xffff, b1 = b0 + (rbl[rt][hf] >> 16);
+          with_row_len(wl[rt][hf], [&](auto lc) {
+            sm = lds_row_spmm<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
+          });
+          if (k >= 1) {
+            const float4 p = tm1[rt][hf];
+            sm = make_float4(2.f * sm.x - p.x, 2.f * sm.y - p.y, 2.f * sm.z - p.z, 2.f * sm.w - p.w);
+          }
+          nv[rt][hf] = sm;
+        }
+      __syncthreads();  // every gather and contraction read of T_k done
+      float* pl = A.basis + int64_t(k + 1) * A.plane;
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          if (!rvS[rt][hf]) continue;
+          float4* own = reinterpret_cast<float4*>(slot + rowS[rt][hf] * kGQ16 + 4 * qs);
+          tm1[rt][hf] = *own;
+          *own = nv[rt][hf];
+          *reinterpret_cast<float4*>(pl + (int64_t(n) * M + rowS[rt][hf]) * Fin + c0) = nv[rt][hf];
+        }
       __syncthreads();
     }
   }
@@ -339,6 +495,24 @@ size_t grp_fwd_lds(int M, int K, int Fout, int64_t nnz) {
          align16(size_t(nnz) * 2);
 }
 
+size_t grp16_fwd_lds(int M, int K, int Fout, int64_t nnz) {
+  const int NOT = Fout <= 32 ? 1 : 2;
+  return size_t(rup(M + 1, 32)) * kGQ16 * 4 + size_t(K) * 512 * NOT * 4 + size_t(nnz) * 4 +
+         align16(size_t(nnz) * 2);
+}
+
+// the 16-channel forward serves Fin % 16 == 0, Fout <= 32 when its LDS fits
+// (CG_GRP16=0 in the environment keeps the 8-channel one, for A/B runs).  A
+// 16-channel one-slot Clenshaw kernel (dx bitwise the same) was measured
+// slower than the 8-channel one on config R (160 vs 148 us) and dropped.
+static bool grp16_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CG_GRP16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 size_t grp_clen_lds(int M, int64_t nnzT) {
   return size_t(2) * rup(M + 1, 32) * kGQ * 4 + size_t(nnzT) * 4 + align16(size_t(nnzT) * 2);
 }
@@ -361,11 +535,18 @@ hipError_t launch_grp_fwd(const int* rowptr, const int* col, const float* val, c
                           float* basis, float* yp, const float* res, int act, float* y,
                           hipStream_t s) {
   if (!grp_ok(M, nnz, Fin, K, Fout)) return hipErrorInvalidValue;
-  const int G = Fin / kGQ;
+  const bool g16 = grp16_enabled() && Fin % kGQ16 == 0 && Fout <= 32 && nnz < 65536 &&
+                   grp16_fwd_lds(M, K, Fout, nnz) <= size_t(kLdsBytes);
+  const int G = Fin / (g16 ? kGQ16 : kGQ);
   GrpFwdArgs a{rowptr, col, val, order, M, rup(M + 1, 32), Fin, K, Fout, N, int(nnz), G, x, W, basis,
                int64_t(N) * M * Fin, y ? yp : nullptr};
-  const size_t lds = grp_fwd_lds(M, K, Fout, nnz);
-  if (Fout <= 32) {
+  const size_t lds = g16 ? grp16_fwd_lds(M, K, Fout, nnz) : grp_fwd_lds(M, K, Fout, nnz);
+  if (g16 && Fout <= 32) {
+    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp16_fwd<1>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (at != hipSuccess) return at;
+    hipLaunchKernelGGL(k_grp16_fwd<1>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+  } else if (Fout <= 32) {
     static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_fwd<1>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (at != hipSuccess) return at;

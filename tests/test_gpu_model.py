@@ -139,6 +139,13 @@ def test_resgnn_humanflow_shape_train_steps_vs_oracle(dev):
     # updated weights are ill-conditioned in the gradients' rounding at K = 20:
     # the oracle recomputes loss and gradients from the GPU's weights of each
     # step, and the update is checked as the oracle's Adam of the GPU gradient
+    # The gradients compose ten K = 20 filters (each output within the 1e-5
+    # filter bar, test_gpu_parity / test_gpu_basis_layout) through the ReLUs
+    # and residual adds.  Contracting in 16- instead of 8-channel groups moves
+    # a hidden layer's y by 7.8e-7 (basis, dx, dW bitwise equal:
+    # scripts/grp16_check.py) and these gradients by up to 3.4e-5 against the
+    # float64 oracle, so they get 5e-5
+    GTOL = 5e-5
     state = [(np.zeros_like(f64(w)), np.zeros_like(f64(w))) for w in model.W]
     for step in range(1, 4):
         Wprev = [f64(w) for w in model.W]
@@ -148,7 +155,7 @@ def test_resgnn_humanflow_shape_train_steps_vs_oracle(dev):
         rl, rdW, _, _ = MO.train_step(x.astype(np.float64), labels, Wprev, lap, K, R, state, step, lr)
         assert abs(float(loss.item()) - rl) <= 1e-5 * rl, (step, float(loss.item()), rl)
         for name, g, rg in zip(model.names, model.dW, rdW):
-            assert O.normwise_err(f64(g), rg) < TOL, (step, name)
+            assert O.normwise_err(f64(g), rg) < GTOL, (step, name)
         new_state = []
         for name, w, w0, g, (m, v) in zip(model.names, model.W, Wprev, model.dW, state):
             rw, m2, v2 = O.adam_step(w0, f64(g), m, v, step, lr=lr)
