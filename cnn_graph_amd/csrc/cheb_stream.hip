@@ -575,8 +575,11 @@ constexpr int kDwNA = 2;      // basis pieces per lane and staged row (64 lanes 
 // dy pieces per lane and staged row: Fout <= 256 either way
 template <int VW> constexpr int dw_nb() { return VW == 4 ? 1 : 4; }
 
-template <int VW>  // 4: float4 pieces (FinK, Fout, pl_fin multiples of 4), 1: floats
-__global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basis,
+// NW waves per block (4 or 8): wave w stages rows w*(16/NW) .. of a batch and
+// accumulates tiles w, w+NW, ..; a tile's MFMA sequence over the rows is the
+// same whatever NW, so the slabs are bitwise independent of it.
+template <int VW, int NW>  // VW 4: float4 pieces (FinK, Fout, pl_fin multiples of 4), 1: floats
+__global__ __launch_bounds__(64 * NW) void k_dw_slabs(const float* __restrict__ basis,
                                                   const float* __restrict__ dy, int64_t R,
                                                   int FinK, int Fout, int64_t rows_per_chunk,
                                                   float* __restrict__ slab, int pl_fin,
@@ -602,8 +605,8 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
   float* s_b = sm + kDwRB * SA;  // [kDwRB][SB]
   const int64_t c0 = int64_t(blockIdx.x) * rows_per_chunk;
   const int64_t c1 = (c0 + rows_per_chunk < R) ? c0 + rows_per_chunk : R;
-  for (int e = threadIdx.x; e < kDwRB * SA; e += 256) s_a[e] = 0.f;  // padding columns
-  for (int e = threadIdx.x; e < kDwRB * SB; e += 256) s_b[e] = 0.f;
+  for (int e = threadIdx.x; e < kDwRB * SA; e += 64 * NW) s_a[e] = 0.f;  // padding columns
+  for (int e = threadIdx.x; e < kDwRB * SB; e += 64 * NW) s_b[e] = 0.f;
   // this lane's pieces of a staged row: basis columns jlo + VW*(lane + 64 i),
   // dy columns VW*(lane + 64 i); their offsets from the row's base
   int64_t aoff[kDwNA];
@@ -623,12 +626,13 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
   const int xcol = FinKh + lane;
   const bool xv = xb && lane <= nxc && xcol >= jlo && xcol < jhi;
   const int64_t xoff = lane < nxc ? int64_t(lane / x_fin) * x_stride + lane % x_fin : 0;
-  V ra[4][kDwNA], rbv[4][kDwNB];
-  float rx[4];
-  auto fetch = [&](int64_t rb) {  // rows rb + 4w .. rb + 4w + 3 into registers
+  constexpr int NR = kDwRB / NW;  // rows per wave and batch
+  V ra[NR][kDwNA], rbv[NR][kDwNB];
+  float rx[NR];
+  auto fetch = [&](int64_t rb) {  // rows rb + NR w .. rb + NR w + NR - 1 into registers
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t rr = rb + 4 * w + q;
+    for (int q = 0; q < NR; ++q) {
+      const int64_t rr = rb + NR * w + q;
       const bool rv = rr < c1;
       if (xv) rx[q] = lane == nxc ? 1.f : rv ? xb[xoff + rr * x_fin] : 0.f;
 #pragma unroll
@@ -641,9 +645,9 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
   };
   auto stage = [&]() {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float* da = s_a + (4 * w + q) * SA;
-      float* db = s_b + (4 * w + q) * SB;
+    for (int q = 0; q < NR; ++q) {
+      float* da = s_a + (NR * w + q) * SA;
+      float* db = s_b + (NR * w + q) * SB;
       if (xv) da[xcol - jlo] = rx[q];
 #pragma unroll
       for (int i = 0; i < kDwNA; ++i)
@@ -661,9 +665,10 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
         }
     }
   };
-  f32x16 acc[kDwTiles / 4];
+  constexpr int NT = kDwTiles / NW;  // tiles per wave
+  f32x16 acc[NT];
 #pragma unroll
-  for (int a = 0; a < kDwTiles / 4; ++a)
+  for (int a = 0; a < NT; ++a)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
   __syncthreads();  // padding zeroed before the first stage
@@ -673,8 +678,8 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
     __syncthreads();
     if (rb + kDwRB < c1) fetch(rb + kDwRB);  // in flight during the MFMAs
 #pragma unroll
-    for (int a = 0; a < kDwTiles / 4; ++a) {
-      const int t = t0 + w + 4 * a;
+    for (int a = 0; a < NT; ++a) {
+      const int t = t0 + w + NW * a;
       if (t < t1) {
         const int jt = t / ftl, ft = t - jt * ftl;
         const float* pa = s_a + h * SA + (jt * 32 - jlo) + li;
@@ -687,8 +692,8 @@ __global__ __launch_bounds__(256) void k_dw_slabs(const float* __restrict__ basi
     __syncthreads();  // the batch buffers are restaged next
   }
 #pragma unroll
-  for (int a = 0; a < kDwTiles / 4; ++a) {
-    const int t = t0 + w + 4 * a;
+  for (int a = 0; a < NT; ++a) {
+    const int t = t0 + w + NW * a;
     if (t >= t1) continue;
     const int jt = t / ftl, ft = t - jt * ftl;
     const int ff = ft * 32 + li;
@@ -919,11 +924,22 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
   }
   const size_t lds = size_t(kDwRB) * ((span | 1) + (((Fout + 31) & ~31) | 1)) * 4;
   const dim3 grid(chunks, groups);
-  if (vw == 4)
-    hipLaunchKernelGGL(k_dw_slabs<4>, grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
+  // 8 waves per block unless CG_DW_WAVES=4 (A/B runs; the slabs are the same)
+  static const int nw = [] {
+    const char* e = getenv("CG_DW_WAVES");
+    return (e && e[0] == '4') ? 4 : 8;
+  }();
+  if (vw == 4 && nw == 8)
+    hipLaunchKernelGGL((k_dw_slabs<4, 8>), grid, dim3(512), lds, s, basis, dy, R, FinK, Fout, rpc,
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
+  else if (vw == 4)
+    hipLaunchKernelGGL((k_dw_slabs<4, 4>), grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
+  else if (nw == 8)
+    hipLaunchKernelGGL((k_dw_slabs<1, 8>), grid, dim3(512), lds, s, basis, dy, R, FinK, Fout, rpc,
                        slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
   else
-    hipLaunchKernelGGL(k_dw_slabs<1>, grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
+    hipLaunchKernelGGL((k_dw_slabs<1, 4>), grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
                        slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
   return hipGetLastError();
 }
