@@ -429,7 +429,7 @@ struct Bwd {
   static constexpr int NU = 2;  // dW MFMAs per recurrence step
   static constexpr int PF = 6;  // dW operand buffers: loads run PF steps ahead
   static constexpr bool OB = DW == 2;
-  static_assert(NU == 2, "the orders-layout dW loads one row quad per step");
+  static_assert(NU == 2 && PF % 2 == 0, "the orders-layout dW loads one row octet per two steps");
 
   const FastBwdArgs& A;
   char* ring;
@@ -459,23 +459,41 @@ struct Bwd {
   }
 
   // Basis row of the wave's MFMA i in lane half h.  Rows layout: rows
-  // dm0 + 2i + h of the wave's chunk.  Orders layout: row quads dealt
-  // round-robin (quad w + 16g to wave w), MFMA 2g + u takes rows
-  // 4(w + 16g) + 2h + u: one 8-byte load per lane feeds both MFMAs of a
-  // step, and in a step the 16 waves read the same 256 contiguous bytes of
-  // each of the 32 planes (the lines are shared in L1 across the waves).
+  // dm0 + 2i + h of the wave's chunk.  Orders layout: row octets dealt
+  // round-robin (octet w + 16g to wave w); step s = i / 2 of octet g = s / 2
+  // takes rows 8(w + 16g) + 4h + 2(s % 2) + i % 2, so ONE 16-byte load per
+  // lane (rows 4h .. 4h+3 of the octet in one plane) feeds the four MFMAs of
+  // two steps: half the load instructions of a per-step 8-byte load, each
+  // still touching the 32 planes
   __device__ __forceinline__ int dw_row(int i) const {
-    return OB ? 4 * (wave + kW * (i >> 1)) + 2 * h + (i & 1) : dm0 + 2 * i + h;
+    return OB ? 8 * (wave + kW * (i >> 2)) + 4 * h + 2 * ((i >> 1) & 1) + (i & 1) : dm0 + 2 * i + h;
+  }
+  // orders layout: the operands of steps s (even) and s + 1 into buffers b0, b1
+  __device__ __forceinline__ void dw_load_oct(int b0, int b1, int s) {
+    const float* dyn = A.dy + size_t(n) * M * Fout;
+    const int jc = imin(li, FinK - 1), fc = imin(li, Fout - 1);
+    const float* bn = A.basis + size_t(n) * FinK * bord;
+    const int m = dw_row(s * NU);  // octet base + 4h (rows < bord: bord is a multiple of 32)
+    const float4 bv = *reinterpret_cast<const float4*>(bn + size_t(jc) * bord + m);
+    da[b0][0] = bv.x;
+    da[b0][1] = bv.y;
+    da[b1][0] = bv.z;
+    da[b1][1] = bv.w;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      db[b0][u] = dyn[size_t(imin(m + u, M - 1)) * Fout + fc];
+      db[b1][u] = dyn[size_t(imin(m + 2 + u, M - 1)) * Fout + fc];
+    }
   }
 
   // ---- fused dW: acc[j][f] += sum over row pairs of basis[m][j] * dy[m][f]
   __device__ __forceinline__ void dw_load(int buf, int i0) {
     const float* dyn = A.dy + size_t(n) * M * Fout;
     const int jc = imin(li, FinK - 1), fc = imin(li, Fout - 1);
-    if (OB) {  // i0 even: rows dw_row(i0) + {0, 1}
+    if (OB) {  // i0 even: rows dw_row(i0) + {0, 1} (the tail after the recurrence)
       const float* bn = A.basis + size_t(n) * FinK * bord;
       const int m = dw_row(i0);
-      const float2 bv = *reinterpret_cast<const float2*>(bn + size_t(jc) * bord + imin(m, bord - 2));
+      const float2 bv = *reinterpret_cast<const float2*>(bn + size_t(jc) * bord + m);
       da[buf][0] = bv.x;
       da[buf][1] = bv.y;
 #pragma unroll
@@ -527,7 +545,14 @@ struct Bwd {
     V a = vzero<V>();
     if (i >= 1) a = r.template reduce<FV, L>(gth);
     if (DW && !CG_DBG(A.dbg, 64)) dw_mfma1(BUF, i * NU, 1, &a);
-    if (DW && !CG_DBG(A.dbg, 128)) dw_load(BUF, (i + PF) * NU);  // refill for step i + PF
+    if (DW && !CG_DBG(A.dbg, 128)) {
+      if (!OB) {
+        dw_load(BUF, (i + PF) * NU);  // refill for step i + PF
+      } else if (BUF & 1) {
+        // odd step: refill steps i + PF - 1 and i + PF (buffers of steps i - 1 and i)
+        dw_load_oct(BUF - 1, BUF, i + PF - 1);
+      }
+    }
     // G_{k+2} of the own row: kept in registers (this thread wrote it two
     // steps ago); debug bit 32 re-reads it from the ring (A/B switch)
     const V p = CG_DBG(A.dbg, 32) ? lds_v<FV>(ring + r.rr + NX2 * 4 * FV) : g2;
@@ -560,11 +585,11 @@ struct Bwd {
     g1 = vzero<V>();
     g2 = g1;
     if (DW) {
-      if (OB) {  // row quads wave, wave + 16, ... (dw_row)
-        const int nq = (M + 3) >> 2;
+      if (OB) {  // row octets wave, wave + 16, ... (dw_row)
+        const int no = (M + 7) >> 3;
         dm0 = 0;
         dm1 = M;
-        npair = wave < nq ? 2 * ((nq - wave + kW - 1) / kW) : 0;
+        npair = wave < no ? 4 * ((no - wave + kW - 1) / kW) : 0;
       } else {  // rows of this wave: 16 near-equal even-sized chunks of [0, M)
         const int q = ((M + 2 * kW - 1) / (2 * kW)) * 2;
         dm0 = imin(wave * q, M);
@@ -573,8 +598,13 @@ struct Bwd {
       }
 #pragma unroll
       for (int e = 0; e < 16; ++e) dacc[e] = 0.f;
+      if (OB) {
 #pragma unroll
-      for (int b = 0; b < PF; ++b) dw_load(b, b * NU);
+        for (int b = 0; b < PF; b += 2) dw_load_oct(b, b + 1, b);
+      } else {
+#pragma unroll
+        for (int b = 0; b < PF; ++b) dw_load(b, b * NU);
+      }
     }
     __syncthreads();
     CG_TS(A.ts, 3);

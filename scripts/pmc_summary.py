@@ -21,7 +21,8 @@ def short(name):
 
 def main(root, tag=None):
     # the bench configuration these passes ran (bench.py defaults: config B)
-    out = {"config": {"M": 976, "N": 256, "K": 25, "Fin": 1, "Fout": 32},
+    layout = os.environ.get("CG_BENCH_LAYOUT", "orders")  # bench.py's default --basis-layout
+    out = {"config": {"M": 976, "N": 256, "K": 25, "Fin": 1, "Fout": 32, "layout": layout},
            "source": f"rocprofv3 passes of `bench.py --steps 50 --warmup 10` ({tag or root})",
            "kernels": {}, "counters": {}}
     for f in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True):
