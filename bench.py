@@ -231,6 +231,10 @@ def main():
                     help="separate cg_adam_update launch even with no exchange step (ablation)")
     ap.add_argument("--force-allreduce", action="store_true",
                     help="run the gradient exchange even at N=1 (1-rank RCCL; overhead study)")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="capture the K timed steps into one HIP graph before the timed region "
+                         "(auto: on at N=1); the timed region replays it (every kernel of every "
+                         "step still runs)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -282,7 +286,7 @@ def main():
     if exchange and args.allreduce == "rccl":
         comm = cdist.RcclComm(local)
         ar_fn = _lib.lib().cg_allreduce_sum_f32
-        ar_args = (comm.handle, runner.dW.data_ptr(), runner.dW.numel(), stream)
+        ar_args = (comm.handle, runner.dW.data_ptr(), runner.dW.numel())
         # proof that the timed exchange spans every rank (ncclCommCount)
         rccl_nranks = comm.nranks()
         if rccl_nranks != world:
@@ -300,7 +304,7 @@ def main():
     mb = [m_adam, torch.zeros_like(W)]
     vb = [v_adam, torch.zeros_like(W)]
 
-    def step(i):
+    def step(i, stream=stream):
         if fwd_adam:
             if i == 0:
                 runner.forward(x, Wb[0], stream=stream)
@@ -319,7 +323,7 @@ def main():
         runner.backward(dy, Wc, stream=stream)
         if exchange:
             if comm is not None:
-                st = ar_fn(*ar_args)
+                st = ar_fn(*ar_args, stream)
                 if st:
                     _lib.check("cg_allreduce_sum_f32", st)
             else:
@@ -328,6 +332,14 @@ def main():
             st = adam(*adam_args, i + 1, scale, stream)
             if st:
                 _lib.check("cg_adam_update", st)
+
+    # HIP graph of the K timed steps (captured untimed, after the warmup): the
+    # timed region is one replay, so the host's per-launch cost (ctypes + the
+    # HIP launch path, ~2 launches per step) no longer sits in front of the
+    # first kernel or between steps.  Each step keeps its own Adam step count.
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1
+                                       and not (exchange and args.allreduce == "torch"))
+    graph = None
 
     def check_comm():
         """After a failed step: poll RCCL's asynchronous error
@@ -341,12 +353,23 @@ def main():
         for i in range(args.warmup):
             step(i)
         torch.cuda.synchronize()
+        if use_graph:
+            graph = torch.cuda.CUDAGraph()
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.graph(graph, stream=cap):
+                for i in range(args.steps):
+                    step(args.warmup + i, stream=cap.cuda_stream)
+            torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(args.steps):
-            step(args.warmup + i)
+        if graph is not None:
+            graph.replay()
+        else:
+            for i in range(args.steps):
+                step(args.warmup + i)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -429,6 +452,8 @@ def main():
                    "parallelism": f"dp{world}",
                    "allreduce": (args.allreduce if exchange else None),
                    "rccl_nranks": rccl_nranks,
+                   "launch": ("one HIP graph replay of the K captured steps" if graph is not None
+                              else "eager C-ABI calls per step"),
                    "adam": ("fused into the dW reduction (cg_cheb_backward_adam)" if fuse_adam
                             else "applied by the next step's forward (cg_cheb_forward_adam)"
                             if fwd_adam else "cg_adam_update")},

@@ -100,7 +100,11 @@ __global__ __launch_bounds__(256) void k_mse_part(const float* __restrict__ pred
 
 // ema (optional, float[3] = {biased, average, local_step}): TF-1.x
 // ExponentialMovingAverage(decay).apply([loss]) of a Tensor, i.e.
-// assign_moving_average(zero_debias=True) (moving_averages.py):
+// assign_moving_average(zero_debias=True) (moving_averages.py).  TF version assumption: the
+// reference pins only "tensorflow-gpu" (requirements.txt:7) and its notebooks ran Python
+// 3.4-3.6 (2017, TF 1.0-1.3), where apply() zero-debiases every Tensor average; TF >= 1.4
+// added ExponentialMovingAverage(zero_debias=False) and would give 0.1*loss after step 1.
+// Parity of this choice is unpinned (no TF in the image):
 //   d1 = 1 - decay; biased -= (biased - loss) * d1; step += 1;
 //   average -= average - biased / (1 - (1 - d1)^step)
 __global__ __launch_bounds__(256) void k_mse_final(const float* __restrict__ slab, int nslab,

@@ -191,7 +191,9 @@ int cg_mse_loss(const float* pred, const float* labels, int64_t n, float* loss, 
                 void* workspace, size_t ws_bytes, void* stream);
 /* The same, and the loss moving average of lib/graph_model.py:265-273
  * (tf.train.ExponentialMovingAverage(decay).apply([loss]), zero-debiased as TF
- * does for a Tensor): ema = device float[3] {biased, average, local_step},
+ * 1.0-1.3 does for a Tensor; the reference pins no TF version, its notebooks are
+ * Python 3.4-3.6 / 2017; TF >= 1.4's zero_debias=False default is NOT what this
+ * computes -- unpinned): ema = device float[3] {biased, average, local_step},
  * zero-initialised by the caller, updated in place; average is loss_average. */
 int cg_mse_loss_ema(const float* pred, const float* labels, int64_t n, float* loss, float* dpred,
                     float* ema, float decay, void* workspace, size_t ws_bytes, void* stream);

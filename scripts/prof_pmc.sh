@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 TAG=${1:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-BENCH="bench.py --steps 50 --warmup 10 --no-cpu-baseline"
+BENCH="bench.py --steps 50 --warmup 10 --no-cpu-baseline --graph off"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 $BENCH > $OUT/kt.log 2>&1 || { echo KT_FAIL; tail -20 $OUT/kt.log; exit 1; }
 for C in FETCH_SIZE WRITE_SIZE "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS" "TCC_HIT_sum TCC_MISS_sum" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   N=$(echo $C | tr ' ' '_')
