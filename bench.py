@@ -17,10 +17,10 @@ ranks (lib/graph_model.py:296-298 is where the exchange sits in the reference).
 
 The timed loop issues exactly those C-ABI calls on torch's current stream
 (ctypes, pre-bound arguments, no per-step allocation or event), bracketed by
-barrier + synchronize; the max over ranks is reported.  After it, each kernel
-is timed alone in bursts of back-to-back launches with HIP events recorded on
-the same stream (roofline.achieved); rocprofv3 summaries of the same command
-live under profiles/ (scripts/prof_pmc.sh), whose PMC-measured HBM bytes of
+barrier + synchronize; the max over ranks is reported.  Before the warmup,
+each kernel is timed alone in bursts of back-to-back launches with HIP events
+recorded on the same stream (roofline.achieved); rocprofv3 summaries of the
+same command live under profiles/ (scripts/prof_pmc.sh), whose PMC-measured HBM bytes of
 the dominant kernel are reported as roofline.traffic when they match this
 configuration.
 
@@ -231,10 +231,10 @@ def main():
                     help="separate cg_adam_update launch even with no exchange step (ablation)")
     ap.add_argument("--force-allreduce", action="store_true",
                     help="run the gradient exchange even at N=1 (1-rank RCCL; overhead study)")
-    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="capture the K timed steps into one HIP graph before the timed region "
-                         "(auto: on at N=1); the timed region replays it (every kernel of every "
-                         "step still runs)")
+    ap.add_argument("--graph", default="off", choices=["on", "off"],
+                    help="capture the K timed steps into one HIP graph before the timed region and "
+                         "replay it there (every kernel of every step still runs); measured 0-1 %% "
+                         "slower than eager launches on config B (profiles/r03_graph), so off")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -337,8 +337,7 @@ def main():
     # timed region is one replay, so the host's per-launch cost (ctypes + the
     # HIP launch path, ~2 launches per step) no longer sits in front of the
     # first kernel or between steps.  Each step keeps its own Adam step count.
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1
-                                       and not (exchange and args.allreduce == "torch"))
+    use_graph = args.graph == "on" and not (exchange and args.allreduce == "torch")
     graph = None
 
     def check_comm():
@@ -348,6 +347,15 @@ def main():
             st = comm.async_error(abort=True)
             if st:
                 sys.exit(f"bench.py: RCCL asynchronous error {st} on rank {rank}")
+
+    # per-kernel timing (roofline.achieved): forward = one kernel; backward =
+    # the recurrence kernel + the tiny fixed-order dW slab reduce.  Run BEFORE
+    # the warmup: ~12 ms of back-to-back launches that also bring the GPU out
+    # of its idle clock state, which otherwise lasts through a short timed
+    # region (driver's 20-step run: steps at 0.060 ms that settle at 0.057 ms
+    # after ~200 steps, profiles/r03_graph).  They touch no training state.
+    fwd_ms = burst_ms(lambda: runner.forward(x, W, stream=stream))
+    bwd_ms = burst_ms(lambda: runner.backward(dy, W, stream=stream))
 
     try:
         for i in range(args.warmup):
@@ -405,10 +413,6 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         med_ms, p90_ms = (float(v) for v in tt.tolist())
 
-    # per-kernel timing (after the timed region): forward = one kernel;
-    # backward = the recurrence kernel + the tiny fixed-order dW slab reduce
-    fwd_ms = burst_ms(lambda: runner.forward(x, W, stream=stream))
-    bwd_ms = burst_ms(lambda: runner.backward(dy, W, stream=stream))
     B = N * Fin
     bytes_fwd, bytes_bwd, _csr = algorithmic_bytes(M, plan.nnz, B, K)
     compulsory_fwd = 4 * (N * M * Fin + N * M * Fin * K + N * M * Fout) + 8 * plan.nnz + 4 * (M + 1)
