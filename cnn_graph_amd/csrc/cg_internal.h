@@ -254,6 +254,13 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
                            int64_t nnzT,
                            int N, int M, int Fin, int K, const float* D, float* dx, int dx_acc,
                            hipStream_t s);
+// the same with dBasis = dy W^T computed in the kernel (bitwise the row GEMM's
+// planes; no D planes): Fout 32 or 64 and the W rows fit the LDS (grp_clen_dy_ok)
+bool grp_clen_dy_ok(int M, int64_t nnzT, int K, int Fout);
+hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* tval,
+                              const int* order, int64_t nnzT, int N, int M, int Fin, int K,
+                              int Fout, const float* dy, const float* W, float* dx, int dx_acc,
+                              hipStream_t s);
 
 // C[Mg x Ng] (+)= op(A)[Mg x Kg] * op(B)[Kg x Ng]; fp32 in/out on MFMA f32.
 // trans_a: A stored [Kg][lda] (A^T row-major); trans_b: B stored [Ng][ldb].

@@ -905,6 +905,12 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
                                     (k + 2 <= K - 1) ? G(k + 2) : nullptr, G(k), G(k), M, B, 2,
                                     k >= 1 ? 2.f : 1.f, s));
       CG_HIP(cg::launch_vm_to_sm(G(0), N, int64_t(M) * Fin, dx, dx_acc, s));
+    } else if (!stream_ws(plan, N, Fin, K, Fout).wide && use_group(plan, Fin, K, Fout) &&
+               cg::grp_clen_dy_ok(M, plan->nnzT, K, Fout)) {
+      // the whole reverse recurrence in LDS per (sample, 8 channels), dBasis
+      // formed in the kernel from dy and W (no dBasis planes)
+      CG_HIP(cg::launch_grp_clen_dy(plan->trowptr, plan->tcol, plan->tval, plan->tlorder, plan->nnzT,
+                                    N, M, Fin, K, Fout, dy, W, dx, dx_acc, s));
     } else {
       float* dA = reinterpret_cast<float*>(rest);
       const int NM = N * M;

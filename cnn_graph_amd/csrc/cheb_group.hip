@@ -487,6 +487,227 @@ __global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
   }
 }
 
+// k_grp_clen_dy: k_grp_clen with dBasis computed in the kernel instead of read
+// from the k-major planes a separate row GEMM wrote (config R: 237 MB written
+// and 262 MB read back per hidden-layer backward).  For each group of four
+// Chebyshev orders kg .. kg+3 a wave computes, per 32-row tile,
+//   D_k[r][c] = sum_f dy[r][f] W[(c0 + c) K + k][f]
+// as ONE transposed 32x32 MFMA tile (rows (order, channel) = 8 ko + c, columns
+// the tile's graph rows) on v_mfma_f32_32x32x2_f32 with the inner index split
+// exactly as k_rowgemm splits it (lane half h feeds f = h KC2 + s at step s,
+// s ascending from a zero accumulator), so every D value is the same sequence
+// of MFMA operations as the row GEMM's and dx stays bitwise the streaming
+// path's.  The MFMA leaves lane (row n, half h) channels 4h .. 4h+3 of the
+// four orders; ds_bpermute hands them to the recurrence's lane (2n + h).
+// The group's W rows sit in LDS (row stride Fout + 4: the 32 (order, channel)
+// rows of an operand read spread over the banks).  The first order group is
+// formed up front; each later one tile per recurrence step of the group
+// before it, so its MFMAs run under the LDS-bound steps: waves 0-3 issue them
+// before the step's gathers, waves 4-7 (the other wave of each SIMD) after,
+// and the tile's result is handed over at the start of the next step.
+struct GrpClenDyArgs {
+  const int* trowptr;
+  const int* tcol;
+  const float* tval;
+  const int* order;
+  int M, Mr, Fin, K, N, nnz, G, Fout, KC2;
+  const float* dy;  // [N][M][Fout]
+  const float* W;   // [Fin*K][Fout], row fin*K + k
+  float* dx;        // [N][M][Fin]
+  int dx_acc;
+  int pipe;  // 1: the next group's tiles during this group's steps; 0: each group's up front
+};
+
+template <int KC2>  // Fout / 2: the row GEMM's inner half (16 or 32)
+__global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j = lane >> 1, hh = lane & 1;   // recurrence lanes: row j, channels 4hh..
+  const int mi = lane & 31, mh = lane >> 5;  // MFMA lanes: tile row / column mi, half mh
+  int n, g;
+  grp_map(blockIdx.x, A.G, n, g);
+  if (n >= A.N) return;
+  const int M = A.M, K = A.K, Fin = A.Fin;
+  constexpr int Fout = 2 * KC2, NB = KC2 / 4;
+  constexpr int WS = Fout + 4;  // LDS row stride of the staged W rows
+  float* slotA = smem;
+  float* slotB = smem + A.Mr * kGQ;
+  float* s_w = slotB + A.Mr * kGQ;  // [K][8][WS]: W row (c0 + ch) K + k
+  float* s_val = s_w + K * kGQ * WS;
+  unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
+  const int c0 = kGQ * g;
+  for (int e = tid; e < A.nnz; e += kGT) {
+    s_val[e] = A.tval[e];
+    s_col[e] = static_cast<unsigned short>(A.tcol[e]);
+  }
+  for (int e = tid; e < K * kGQ * Fout; e += kGT) {
+    const int f = e % Fout, kc = e / Fout, ch = kc % kGQ, k = kc / kGQ;
+    s_w[kc * WS + f] = A.W[(int64_t(c0 + ch) * K + k) * Fout + f];
+  }
+  int row[kGRT], rb[kGRT], re[kGRT], wl[kGRT];
+  bool rv[kGRT];
+  int drow[kGRT];  // the MFMA lane's tile row (graph row of column mi), -1 past M
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    const int idx = (wave + 8 * rt) * 32 + j;
+    rv[rt] = idx < M;
+    row[rt] = rv[rt] ? A.order[idx] : M;
+    rb[rt] = rv[rt] ? A.trowptr[row[rt]] : 0;
+    re[rt] = rv[rt] ? A.trowptr[row[rt] + 1] : 0;
+    wl[rt] = wave_max(re[rt] - rb[rt]);
+    const int midx = (wave + 8 * rt) * 32 + mi;
+    drow[rt] = midx < M ? A.order[midx] : -1;
+  }
+  if (tid < 2 * kGQ) (tid < kGQ ? slotA : slotB)[M * kGQ + (tid & (kGQ - 1))] = 0.f;  // zero row M
+  __syncthreads();
+  const int bsrc = ((lane >> 1) + 32 * (lane & 1)) * 4;  // ds_bpermute source of lane 2n + h
+  const bool mfma_first = wave < 4;
+  // dy operand of tile rt (the MFMA lane's half row: KC2 floats), loaded ahead
+  // of its MFMAs (global / L2: the sample's dy is read by every group)
+  auto dload = [&](int rt, float4 (&b)[NB]) {
+    const float* dr = A.dy + (int64_t(n) * M + (drow[rt] >= 0 ? drow[rt] : 0)) * Fout + mh * KC2;
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+      b[q] = drow[rt] >= 0 ? *reinterpret_cast<const float4*>(dr + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  // one D tile: orders kg .. kg+3 of a 32-row tile on the MFMA (acc), W from LDS
+  auto dtile = [&](int kg, const float4 (&b)[NB], f32x16& acc) {
+    const int kk = kg + (mi >> 3);
+    const float* wr = s_w + ((kk < K ? kk : 0) * kGQ + (mi & 7)) * WS + mh * KC2;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      float4 a = *reinterpret_cast<const float4*>(wr + 4 * q);
+      if (kk >= K) a = make_float4(0.f, 0.f, 0.f, 0.f);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[q].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[q].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[q].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[q].w, acc, 0, 0, 0);
+    }
+  };
+  // D of the current order group in ONE register array, whose layout
+  // alternates between groups: even groups Dg[rt][ko], odd groups Dg[ko][rt].
+  // Step ko of an even group consumes column [*][ko] and the next (odd)
+  // group's tile rt' = ko lands in that same column ([ko'][rt' = ko]); odd
+  // groups consume and refill rows the same way -- so the next group's tiles
+  // fill exactly the registers the current group has finished with.
+  float Dg[4][4][4];
+  // acc[4 ko + m] at lane (n, h): order kg + ko, channel 4h + m of row n
+  auto handover = [&](const f32x16& acc, int rt, bool odd) {
+#pragma unroll
+    for (int ko = 0; ko < 4; ++ko)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float v = __int_as_float(__builtin_amdgcn_ds_bpermute(bsrc, __float_as_int(acc[4 * ko + m])));
+        if (odd) Dg[ko][rt][m] = v;
+        else Dg[rt][ko][m] = v;
+      }
+  };
+  // G_{k+2} is read back from the slot G_k overwrites (same lane, same row),
+  // so only the latest G lives in registers (G_0 at the end)
+  float G0[kGRT][4];
+  const int ktop = ((K - 1) / 4) * 4;
+  const bool pipe = A.pipe != 0;
+  auto run_group = [&](int kg, auto odd_c) {
+    constexpr bool odd = decltype(odd_c)::value;
+    if (kg == ktop || !pipe) {
+      constexpr int NL = NB <= 4 ? kGRT : 1;  // tiles' dy loads in flight together
+      float4 b[NL][NB];
+#pragma unroll
+      for (int rt = 0; rt < NL; ++rt) dload(rt, b[rt]);
+#pragma unroll
+      for (int rt = 0; rt < kGRT; ++rt) {
+        if (NL == 1 && rt > 0) dload(rt, b[0]);
+        f32x16 a0;
+        dtile(kg, b[NL == 1 ? 0 : rt], a0);
+        handover(a0, rt, odd);
+      }
+    }
+    const bool more = pipe && kg >= 4;  // form the next (lower) order group meanwhile
+    f32x16 acc;
+    float4 pb[NB];  // dy of the next tile, loaded one step ahead
+    if (more) dload(3, pb);
+#pragma unroll
+    for (int ko = 3; ko >= 0; --ko) {
+      const int k = kg + ko;
+      // the next group's tile formed during the previous step (its registers
+      // held orders of this group that are consumed by now)
+      if (more && ko < 3) handover(acc, ko + 1, !odd);
+      const bool step = k < K - 1;  // a recurrence step (k == K-1: the start)
+      if (more && (mfma_first || !step)) {
+        dtile(kg - 4, pb, acc);
+        if (ko > 0) dload(ko - 1, pb);
+      }
+      if (k == K - 1) {
+        // G_{K-1} = D_{K-1} + c * (+0)  (k_clenshaw_step's expression with no G_K)
+        const float cl = (K - 1 >= 1) ? 2.f : 1.f;
+#pragma unroll
+        for (int rt = 0; rt < kGRT; ++rt) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) G0[rt][m] = (odd ? Dg[ko][rt][m] : Dg[rt][ko][m]) + cl * 0.f;
+          if (K > 1 && rv[rt])
+            *reinterpret_cast<float4*>(slotA + row[rt] * kGQ + 4 * hh) =
+                make_float4(G0[rt][0], G0[rt][1], G0[rt][2], G0[rt][3]);
+        }
+        __syncthreads();
+      } else if (step) {
+        const float* cur = ((K - 2 - k) & 1) ? slotB : slotA;
+        float* nxt = ((K - 2 - k) & 1) ? slotA : slotB;
+        const float c = k >= 1 ? 2.f : 1.f;
+#pragma unroll
+        for (int rt = 0; rt < kGRT; ++rt) {
+          float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (rv[rt])
+            with_row_len(wl[rt], [&](auto lc) {
+              sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+            });
+          const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
+          float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kGQ + 4 * hh);
+          float g2[4] = {0.f, 0.f, 0.f, 0.f};
+          if (k + 2 <= K - 1 && rv[rt]) {  // G_{k+2}: this slot, written two steps ago
+            const float4 p = *own;
+            g2[0] = p.x; g2[1] = p.y; g2[2] = p.z; g2[3] = p.w;
+          }
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            float o = (odd ? Dg[ko][rt][m] : Dg[rt][ko][m]) + c * sv[m];
+            if (k + 2 <= K - 1) o = o - g2[m];
+            G0[rt][m] = o;
+          }
+          if (k > 0 && rv[rt]) *own = make_float4(G0[rt][0], G0[rt][1], G0[rt][2], G0[rt][3]);
+        }
+        if (more && !mfma_first) {
+          dtile(kg - 4, pb, acc);
+          if (ko > 0) dload(ko - 1, pb);
+        }
+        if (k > 0) __syncthreads();
+      }
+    }
+    if (more) handover(acc, 0, !odd);
+  };
+  for (int kg = ktop;;) {
+    run_group(kg, IntC<0>{});
+    if (kg < 4) break;
+    kg -= 4;
+    run_group(kg, IntC<1>{});
+    if (kg < 4) break;
+    kg -= 4;
+  }
+#pragma unroll
+  for (int rt = 0; rt < kGRT; ++rt) {
+    if (!rv[rt]) continue;
+    float4* d = reinterpret_cast<float4*>(A.dx + (int64_t(n) * M + row[rt]) * Fin + c0 + 4 * hh);
+    float4 o = make_float4(G0[rt][0], G0[rt][1], G0[rt][2], G0[rt][3]);
+    if (A.dx_acc) {
+      const float4 p = *d;
+      o = make_float4(p.x + o.x, p.y + o.y, p.z + o.z, p.w + o.w);
+    }
+    *d = o;
+  }
+}
+
 }  // namespace
 
 size_t grp_fwd_lds(int M, int K, int Fout, int64_t nnz) {
@@ -579,6 +800,51 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (at != hipSuccess) return at;
   hipLaunchKernelGGL(k_grp_clen, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
+  return hipGetLastError();
+}
+
+// the fused variant serves Fout a multiple of 32 up to 64 (the row GEMM's
+// inner split: KC2 = Fout / 2, a multiple of 16); CG_CLEN_DY=0 in the
+// environment keeps the row GEMM + k_grp_clen pair (A/B runs)
+
+size_t grp_clen_dy_lds(int M, int64_t nnzT, int K, int Fout) {
+  return grp_clen_lds(M, nnzT) + size_t(K) * kGQ * (Fout + 4) * 4;
+}
+
+bool grp_clen_dy_ok(int M, int64_t nnzT, int K, int Fout) {
+  static const bool on = [] {
+    const char* e = getenv("CG_CLEN_DY");
+    return !(e && e[0] == '0');
+  }();
+  return on && (Fout == 32 || Fout == 64) && M <= kGRT * 8 * 32 &&
+         grp_clen_dy_lds(M, nnzT, K, Fout) <= size_t(kLdsBytes);
+}
+
+hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* tval,
+                              const int* order, int64_t nnzT, int N, int M, int Fin, int K,
+                              int Fout, const float* dy, const float* W, float* dx, int dx_acc,
+                              hipStream_t s) {
+  if (Fin % kGQ || K < 1 || !grp_clen_dy_ok(M, nnzT, K, Fout))
+    return hipErrorInvalidValue;
+  const int G = Fin / kGQ;
+  static const int pipe = [] {  // CG_CLEN_DY=2: each group's tiles up front (A/B runs)
+    const char* e = getenv("CG_CLEN_DY");
+    return (e && e[0] == '2') ? 0 : 1;
+  }();
+  GrpClenDyArgs a{trowptr, tcol, tval, order, M, rup(M + 1, 32), Fin, K, N, int(nnzT), G, Fout,
+                  Fout / 2, dy, W, dx, dx_acc, pipe};
+  static hipError_t at16 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen_dy<16>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+  static hipError_t at32 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen_dy<32>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+  const size_t lds = grp_clen_dy_lds(M, nnzT, K, Fout);
+  if (Fout == 32) {
+    if (at16 != hipSuccess) return at16;
+    hipLaunchKernelGGL(k_grp_clen_dy<16>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+  } else {
+    if (at32 != hipSuccess) return at32;
+    hipLaunchKernelGGL(k_grp_clen_dy<32>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+  }
   return hipGetLastError();
 }
 
