@@ -17,9 +17,10 @@ ranks (lib/graph_model.py:296-298 is where the exchange sits in the reference).
 
 The timed loop issues exactly those C-ABI calls on torch's current stream
 (ctypes, pre-bound arguments, no per-step allocation or event), bracketed by
-barrier + synchronize; the max over ranks is reported.  Before the warmup,
-each kernel is timed alone in bursts of back-to-back launches with HIP events
-recorded on the same stream (roofline.achieved); rocprofv3 summaries of the
+barrier + synchronize; the max over ranks is reported.  After it, each kernel
+is timed alone in bursts of back-to-back launches with HIP events recorded on
+the same stream (roofline.achieved; the same bursts also run once before the
+warmup to lift the GPU out of its idle clocks); rocprofv3 summaries of the
 same command live under profiles/ (scripts/prof_pmc.sh), whose PMC-measured HBM bytes of
 the dominant kernel are reported as roofline.traffic when they match this
 configuration.
@@ -348,14 +349,14 @@ def main():
             if st:
                 sys.exit(f"bench.py: RCCL asynchronous error {st} on rank {rank}")
 
-    # per-kernel timing (roofline.achieved): forward = one kernel; backward =
-    # the recurrence kernel + the tiny fixed-order dW slab reduce.  Run BEFORE
-    # the warmup: ~12 ms of back-to-back launches that also bring the GPU out
-    # of its idle clock state, which otherwise lasts through a short timed
-    # region (driver's 20-step run: steps at 0.060 ms that settle at 0.057 ms
-    # after ~200 steps, profiles/r03_graph).  They touch no training state.
-    fwd_ms = burst_ms(lambda: runner.forward(x, W, stream=stream))
-    bwd_ms = burst_ms(lambda: runner.backward(dy, W, stream=stream))
+    # Before the warmup: ~12 ms of back-to-back forward / backward launches
+    # (the per-kernel timing bursts below, results discarded) that bring the
+    # GPU out of its idle clock state, which otherwise lasts through a short
+    # timed region (driver's 20-step run: steps at 0.060 ms that settle at
+    # 0.057 ms after ~200 steps, profiles/r03_graph).  They touch no training
+    # state.  The kernel timings themselves are taken after the timed region.
+    burst_ms(lambda: runner.forward(x, W, stream=stream))
+    burst_ms(lambda: runner.backward(dy, W, stream=stream))
 
     try:
         for i in range(args.warmup):
@@ -413,6 +414,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         med_ms, p90_ms = (float(v) for v in tt.tolist())
 
+    # per-kernel timing (roofline.achieved), on the warm GPU: forward = one
+    # kernel; backward = the recurrence kernel + the tiny fixed-order dW slab reduce
+    fwd_ms = burst_ms(lambda: runner.forward(x, W, stream=stream))
+    bwd_ms = burst_ms(lambda: runner.backward(dy, W, stream=stream))
     B = N * Fin
     bytes_fwd, bytes_bwd, _csr = algorithmic_bytes(M, plan.nnz, B, K)
     compulsory_fwd = 4 * (N * M * Fin + N * M * Fin * K + N * M * Fout) + 8 * plan.nnz + 4 * (M + 1)

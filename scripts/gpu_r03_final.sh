@@ -24,4 +24,12 @@ echo PMC_OK
 timeout -k 10 400 python3 scripts/bench_configs.py C1 C2 E R > $O/configs.jsonl 2> $O/configs.err && cut -c1-220 $O/configs.jsonl || exit 1
 timeout -k 10 400 python3 scripts/bench_configs.py D --d-batch 256 --layout planes > $O/D256.jsonl 2> $O/D256.err && cut -c1-260 $O/D256.jsonl || exit 1
 bash scripts/gpu_r03_profER.sh $TAG/prof R > $O/profR.log 2>&1 || { tail -20 $O/profR.log; exit 1; }
+
+# A/B: act stores staged through LDS (CG_SEQ_STAGE 1, default) vs per lane (0), config E
+for rep in 1 2; do
+  for v in 1 0; do
+    CG_SEQ_STAGE=$v timeout -k 10 200 python3 scripts/bench_configs.py E >> $O/E_stage$v.jsonl 2>> $O/E_stage.err || exit 1
+  done
+done
+for v in 1 0; do echo "== stage $v"; cut -c1-200 $O/E_stage$v.jsonl; done
 echo DONE
