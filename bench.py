@@ -240,6 +240,12 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    # ONE JSON line on stdout: whatever the libraries print there (RCCL's
+    # version banner at communicator init goes to stdout) is sent to stderr,
+    # and the result line is written to the saved stdout descriptor
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
@@ -494,7 +500,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(L, fake, K, Fout, seconds=args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        ctypes.CDLL(None).fflush(None)  # library stdio buffers: still to stderr
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if comm is not None:
         torch.cuda.synchronize()
         comm.close()

@@ -721,8 +721,19 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
   const int64_t i = int64_t(blockIdx.x) * 64 + lane;
   float s = 0.f;
   if (i < count) {
-#pragma unroll 8
-    for (int z = w; z < nslab; z += 16) s = s + slab[int64_t(z) * count + i];
+    // this lane's slabs z = w, w + 16, ..: up to 16 loads in flight at once,
+    // then added in order (the same order as one load per add)
+    for (int z0 = w; z0 < nslab; z0 += 256) {
+      float vz[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int z = z0 + 16 * q;
+        vz[q] = z < nslab ? slab[int64_t(z) * count + i] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (z0 + 16 * q < nslab) s = s + vz[q];
+    }
   }
   part[w][lane] = s;
   __syncthreads();

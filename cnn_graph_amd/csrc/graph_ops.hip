@@ -139,10 +139,28 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs_adam(const float* __restr
   __shared__ float part[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t i = int64_t(blockIdx.x) * 64 + lane;
+  // wave 0's Adam operands, loaded behind the slab loads instead of after the sum
+  float p0 = 0.f, m0 = 0.f, v0 = 0.f;
+  if (w == 0 && i < count) {
+    p0 = a.param[i];
+    m0 = a.m[i];
+    v0 = a.v[i];
+  }
   float s = 0.f;
   if (i < count) {
-#pragma unroll 8
-    for (int z = w; z < nslab; z += 16) s = s + slab[int64_t(z) * count + i];
+    // this lane's slabs z = w, w + 16, ..: up to 16 loads in flight at once,
+    // then added in order (the same order as one load per add)
+    for (int z0 = w; z0 < nslab; z0 += 256) {
+      float vz[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int z = z0 + 16 * q;
+        vz[q] = z < nslab ? slab[int64_t(z) * count + i] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (z0 + 16 * q < nslab) s = s + vz[q];
+    }
   }
   part[w][lane] = s;
   __syncthreads();
@@ -151,7 +169,10 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs_adam(const float* __restr
 #pragma unroll
     for (int q = 0; q < 16; ++q) t = t + part[q][lane];
     grad[i] = t;
-    adam_elem(a.param, a.m, a.v, i, t, a.grad_scale, a.lr_t, a.beta1, a.beta2, a.eps);
+    const AdamElem r = adam_math(p0, m0, v0, t, a.grad_scale, a.lr_t, a.beta1, a.beta2, a.eps);
+    a.m[i] = r.m;
+    a.v[i] = r.v;
+    a.param[i] = r.p;
   }
 }
 

@@ -14,10 +14,11 @@ tail -1 $O/pytest.txt
 [ $rc -eq 0 ] || { grep -E "FAIL|Error" $O/pytest.txt | head; exit 1; }
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err || exit 1
 timeout -k 10 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.json 2>> $O/bench.err || exit 1
+for r in 2 3; do timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/bench_$r.json 2>> $O/bench.err || exit 1; done
 timeout -k 10 200 python3 bench.py --force-allreduce --no-cpu-baseline > $O/bench_ar.json 2>> $O/bench.err || exit 1
 timeout -k 10 200 python3 bench.py --graph on --no-cpu-baseline > $O/bench_graph.json 2>> $O/bench.err || exit 1
 python3 -c "
 import json
-for f in ['bench.json', 'bench20.json', 'bench_ar.json', 'bench_graph.json']:
+for f in ['bench.json', 'bench_2.json', 'bench_3.json', 'bench20.json', 'bench_ar.json', 'bench_graph.json']:
     d = json.load(open('$O/' + f)); c = d['config']
     print(f, d['value'], d['ms_per_step'], d['step_ms_median'], d['roofline']['frac'], d['roofline_spmm_fwd']['frac'], c['allreduce'], c['rccl_nranks'], c['adam'][:30], c['launch'])"
