@@ -118,6 +118,14 @@ __device__ __forceinline__ void bst16_sc1(__amdgpu_buffer_rsrc_t r, int off, flo
   __builtin_amdgcn_raw_buffer_store_b128(w, r, off * 4, 0, 16);
 }
 
+static int seq_xpre() {
+  static const int on = [] {
+    const char* e = getenv("CG_SEQ_XPRE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
 struct SeqArgs {
   const int* rowptr;  // L~ (CSR, sorted columns)
   const int* col;
@@ -146,8 +154,11 @@ struct SeqArgs {
                       // 8 no partner wait, 16 no gx / c loads, 32 no plane stores,
                       // 64 no act stores, 128 no c stores, 256 no h stores
   unsigned long long* ts;  // ablation build: phase stamps of step 1 (CG_TS), else NULL
+  int xpre;           // 1: xplanes already hold T_k(x_t) for every step (launch_lstm_seq's
+                      // pre-pass): the x contraction reads them, no x recurrence in the loop
 };
 
+template <bool XPRE>
 __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -270,7 +281,30 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           }
         }
       };
-      if (A.xs) {
+      if (XPRE) {
+        // the x basis of step t, precomputed for all steps: MFMA step s takes
+        // channel 2s + hh of the lane's rows straight from plane k (L2)
+        const int Fin = A.Fin;
+        for (int k = 0; k < K; ++k) {
+          const float* xp = A.xplanes + int64_t(k) * A.xpstride + (int64_t(t) * N + n) * M * Fin;
+          const float* wq = s_Wx + k * 512 + hh * 64 + j;
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            if (2 * s >= Fin || CG_DBG(A.dbg, 1)) break;
+            const int c = 2 * s + hh;
+            float b[kRT];
+#pragma unroll
+            for (int rt = 0; rt < kRT; ++rt)
+              b[rt] = (rv[rt] && c < Fin) ? xp[int64_t(row[rt]) * Fin + c] : 0.f;
+            const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
+#pragma unroll
+            for (int rt = 0; rt < kRT; ++rt) {
+              acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b[rt], acc[rt][0], 0, 0, 0);
+              acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b[rt], acc[rt][1], 0, 0, 0);
+            }
+          }
+        }
+      } else if (A.xs) {
         // the fused x-conv: the recurrence of x_t (Fin <= 8 channels in one
         // 8-channel slot, the rest zero) and its contraction with Wx; both
         // workgroups run it, workgroup 0 keeps the x basis planes
@@ -766,10 +800,14 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
       (xs && (Fin < 1 || Fin > 8 || !Wx || !xplanes)) || (!xs && !gx))
     return hipErrorInvalidValue;
   // the kernel's static LDS (the abort word) counts against the same 160 KB
-  static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_seq),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               kLdsBytes - kSeqStaticLds);
-  if (attr != hipSuccess) return attr;
+  static hipError_t attr0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_seq<false>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                kLdsBytes - kSeqStaticLds);
+  static hipError_t attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_seq<true>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                kLdsBytes - kSeqStaticLds);
+  if (attr0 != hipSuccess) return attr0;
+  if (attr1 != hipSuccess) return attr1;
   int dev = 0, rate_khz = 0;
   hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
@@ -779,25 +817,44 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
             P % 8 == 0 ? 1 : 0, gx, xs, Wx, xplanes, xpstride, Fin, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
             // a pair hand-off that has not happened after 2 s ends the launch
             static_cast<unsigned long long>(rate_khz) * 2000ull, (debug_flags() >> 16) & 0xff,
-            nullptr};
+            nullptr, 0};
 #ifdef CG_DEBUG
   a.ts = g_debug_ts;
 #endif
   hipError_t e = hipMemsetAsync(flags, 0, sizeof(int) * (size_t(2) * P + 1), s);
   if (e != hipSuccess) return e;
+  // x basis of all T steps up front (plane 0 = x, plane k = T_k(x) by the
+  // streaming steps over the T*N samples: CSR order from +0, the same values
+  // as the in-loop recurrence), unless CG_SEQ_XPRE=0 (A/B runs): the loop
+  // then only contracts them, and neither workgroup of a pair recomputes them
+  if (xs && seq_xpre()) {
+    const int64_t R = int64_t(T) * N * M;
+    e = hipMemcpyAsync(xplanes, xs, size_t(R) * Fin * sizeof(float), hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+    for (int k = 1; k < K; ++k) {
+      e = launch_cheb_step(rowptr, col, val, nullptr, xplanes + int64_t(k - 1) * xpstride,
+                           k >= 2 ? xplanes + int64_t(k - 2) * xpstride : nullptr,
+                           xplanes + int64_t(k) * xpstride, nullptr, nullptr, nullptr, T * N, M, Fin,
+                           K, k, false, s);
+      if (e != hipSuccess) return e;
+    }
+    a.xpre = 1;
+  }
   // a pair waits for its partner, so every workgroup of the grid must be
   // resident at once: check the grid against the occupancy query (what a
   // cooperative launch would check, MI355X_MICROARCH.md §Residency), with one
   // workgroup per CU of margin, then launch plainly
   const size_t lds = lstm_seq_lds(M, K, nnz, xs ? Fin : 0);
   int per_cu = 0, cus = 0;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_lstm_seq),
-                                                   kST, lds);
+  const void* kern = a.xpre ? reinterpret_cast<const void*>(&k_lstm_seq<true>)
+                            : reinterpret_cast<const void*>(&k_lstm_seq<false>);
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kST, lds);
   if (e != hipSuccess) return e;
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
   if (per_cu < 1 || 2 * P > per_cu * cus) return hipErrorCooperativeLaunchTooLarge;
-  hipLaunchKernelGGL(k_lstm_seq, dim3(2 * P), dim3(kST), lds, s, a);
+  if (a.xpre) hipLaunchKernelGGL(k_lstm_seq<true>, dim3(2 * P), dim3(kST), lds, s, a);
+  else hipLaunchKernelGGL(k_lstm_seq<false>, dim3(2 * P), dim3(kST), lds, s, a);
   return hipGetLastError();
 }
 
