@@ -20,5 +20,6 @@ timeout -k 10 200 python3 bench.py --graph on --no-cpu-baseline > $O/bench_graph
 python3 -c "
 import json
 for f in ['bench.json', 'bench_2.json', 'bench_3.json', 'bench20.json', 'bench_ar.json', 'bench_graph.json']:
-    d = json.load(open('$O/' + f)); c = d['config']
+    d = [json.loads(l) for l in open('$O/' + f) if l.startswith('{')][0]; c = d['config']
     print(f, d['value'], d['ms_per_step'], d['step_ms_median'], d['roofline']['frac'], d['roofline_spmm_fwd']['frac'], c['allreduce'], c['rccl_nranks'], c['adam'][:30], c['launch'])"
+timeout -k 10 400 python3 scripts/bench_configs.py C1 C2 E R > $O/configs.jsonl 2> $O/configs.err && cut -c1-220 $O/configs.jsonl
