@@ -529,7 +529,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
   grp_map(blockIdx.x, A.G, n, g);
   if (n >= A.N) return;
   const int M = A.M, K = A.K, Fin = A.Fin;
-  constexpr int Fout = 2 * KC2, NB = KC2 / 4;
+  constexpr int Fout = 2 * KC2;
   constexpr int WS = Fout + 4;  // LDS row stride of the staged W rows
   float* slotA = smem;
   float* slotB = smem + A.Mr * kGQ;
@@ -565,26 +565,30 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
   const bool mfma_first = wave < 4;
   // dy operand of tile rt (the MFMA lane's half row: KC2 floats), loaded ahead
   // of its MFMAs (global / L2: the sample's dy is read by every group)
-  auto dload = [&](int rt, float4 (&b)[NB]) {
+  auto dload = [&](int rt, float (&b)[KC2]) {
     const float* dr = A.dy + (int64_t(n) * M + (drow[rt] >= 0 ? drow[rt] : 0)) * Fout + mh * KC2;
+    if constexpr (KC2 % 4 == 0) {
 #pragma unroll
-    for (int q = 0; q < NB; ++q)
-      b[q] = drow[rt] >= 0 ? *reinterpret_cast<const float4*>(dr + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = 0; q < KC2 / 4; ++q) {
+        const float4 v = drow[rt] >= 0 ? *reinterpret_cast<const float4*>(dr + 4 * q)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < KC2; ++q) b[q] = drow[rt] >= 0 ? dr[q] : 0.f;
+    }
   };
   // one D tile: orders kg .. kg+3 of a 32-row tile on the MFMA (acc), W from LDS
-  auto dtile = [&](int kg, const float4 (&b)[NB], f32x16& acc) {
+  auto dtile = [&](int kg, const float (&b)[KC2], f32x16& acc) {
     const int kk = kg + (mi >> 3);
     const float* wr = s_w + ((kk < K ? kk : 0) * kGQ + (mi & 7)) * WS + mh * KC2;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      float4 a = *reinterpret_cast<const float4*>(wr + 4 * q);
-      if (kk >= K) a = make_float4(0.f, 0.f, 0.f, 0.f);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b[q].x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b[q].y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b[q].z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b[q].w, acc, 0, 0, 0);
+    for (int q = 0; q < KC2; ++q) {
+      const float a = kk < K ? wr[q] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b[q], acc, 0, 0, 0);
     }
   };
   // D of the current order group in ONE register array, whose layout
@@ -613,8 +617,8 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
   auto run_group = [&](int kg, auto odd_c) {
     constexpr bool odd = decltype(odd_c)::value;
     if (kg == ktop || !pipe) {
-      constexpr int NL = NB <= 4 ? kGRT : 1;  // tiles' dy loads in flight together
-      float4 b[NL][NB];
+      constexpr int NL = KC2 <= 16 ? kGRT : 1;  // tiles' dy loads in flight together
+      float b[NL][KC2];
 #pragma unroll
       for (int rt = 0; rt < NL; ++rt) dload(rt, b[rt]);
 #pragma unroll
@@ -627,7 +631,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
     }
     const bool more = pipe && kg >= 4;  // form the next (lower) order group meanwhile
     f32x16 acc;
-    float4 pb[NB];  // dy of the next tile, loaded one step ahead
+    float pb[KC2];  // dy of the next tile, loaded one step ahead
     if (more) dload(3, pb);
 #pragma unroll
     for (int ko = 3; ko >= 0; --ko) {
@@ -803,9 +807,9 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
   return hipGetLastError();
 }
 
-// the fused variant serves Fout a multiple of 32 up to 64 (the row GEMM's
-// inner split: KC2 = Fout / 2, a multiple of 16); CG_CLEN_DY=0 in the
-// environment keeps the row GEMM + k_grp_clen pair (A/B runs)
+// the fused variant serves Fout 2, 32 and 64 (the row GEMM's inner split
+// KC2 = Fout / 2: 1, 16, 32 -- the ResGNN's output layer and hidden layers);
+// CG_CLEN_DY=0 in the environment keeps the row GEMM + k_grp_clen pair (A/B runs)
 
 size_t grp_clen_dy_lds(int M, int64_t nnzT, int K, int Fout) {
   return grp_clen_lds(M, nnzT) + size_t(K) * kGQ * (Fout + 4) * 4;
@@ -816,7 +820,7 @@ bool grp_clen_dy_ok(int M, int64_t nnzT, int K, int Fout) {
     const char* e = getenv("CG_CLEN_DY");
     return !(e && e[0] == '0');
   }();
-  return on && (Fout == 32 || Fout == 64) && M <= kGRT * 8 * 32 &&
+  return on && (Fout == 2 || Fout == 32 || Fout == 64) && M <= kGRT * 8 * 32 &&
          grp_clen_dy_lds(M, nnzT, K, Fout) <= size_t(kLdsBytes);
 }
 
@@ -838,7 +842,12 @@ hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* 
   static hipError_t at32 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen_dy<32>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   const size_t lds = grp_clen_dy_lds(M, nnzT, K, Fout);
-  if (Fout == 32) {
+  static hipError_t at1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen_dy<1>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+  if (Fout == 2) {
+    if (at1 != hipSuccess) return at1;
+    hipLaunchKernelGGL(k_grp_clen_dy<1>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+  } else if (Fout == 32) {
     if (at16 != hipSuccess) return at16;
     hipLaunchKernelGGL(k_grp_clen_dy<16>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
   } else {

@@ -34,10 +34,12 @@ def _t(a, dev):
 
 # (golden graph, N, Fin, K, Fout): config R's hidden layer (M = 1024, K = 20),
 # a partial order group (K = 7, 2), Fout = 64 (two 16-step chunks per half),
-# a graph whose last row tile is ragged (config B, M = 976)
+# a graph whose last row tile is ragged (config B, M = 976), Fout = 2 (the
+# ResGNN output layer: one MFMA step per tile)
 CASES = [("golden_E.npz", 3, 32, 20, 32), ("golden_E.npz", 2, 16, 7, 64),
          ("golden_E.npz", 4, 8, 2, 32), ("golden_B.npz", 3, 24, 5, 32),
-         ("golden_B.npz", 2, 32, 20, 32), ("golden_B.npz", 2, 8, 1, 32)]
+         ("golden_B.npz", 2, 32, 20, 32), ("golden_B.npz", 2, 8, 1, 32),
+         ("golden_E.npz", 3, 32, 20, 2), ("golden_B.npz", 2, 16, 5, 2)]
 
 
 @pytest.mark.parametrize("gname,N,Fin,K,Fout", CASES)
