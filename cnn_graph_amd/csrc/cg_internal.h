@@ -255,7 +255,7 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
                            int N, int M, int Fin, int K, const float* D, float* dx, int dx_acc,
                            hipStream_t s);
 // the same with dBasis = dy W^T computed in the kernel (bitwise the row GEMM's
-// planes; no D planes): Fout 32 or 64 and the W rows fit the LDS (grp_clen_dy_ok)
+// planes; no D planes): Fout 2, 32 or 64 and the W rows fit the LDS (grp_clen_dy_ok)
 bool grp_clen_dy_ok(int M, int64_t nnzT, int K, int Fout);
 hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* tval,
                               const int* order, int64_t nnzT, int N, int M, int Fin, int K,
