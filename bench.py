@@ -55,6 +55,7 @@ sys.path.insert(0, ROOT)
 from cnn_graph_amd import _lib  # noqa: E402
 from cnn_graph_amd import dist as cdist  # noqa: E402
 from cnn_graph_amd import ops  # noqa: E402
+from cnn_graph_amd.dp_step import ChebTrainStep  # noqa: E402
 from cnn_graph_amd.graph_conv import truncated_normal_  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
@@ -108,13 +109,28 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(L, fake, K, Fout, n=256, seconds=10.0):
+def cpu_pass_times(fn, warmup=10, min_passes=50, seconds=10.0, max_passes=100000):
+    """SURVEY.md §8d's timing rule for the CPU leg: `warmup` untimed passes,
+    then timed passes until at least `min_passes` AND about `seconds` have
+    run (capped by max_passes).  Returns the per-pass times (s)."""
+    for _ in range(warmup):
+        fn()
+    times = []
+    t_end = time.perf_counter() + seconds
+    while len(times) < max_passes and (len(times) < min_passes or time.perf_counter() < t_end):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return times
+
+
+def cpu_baseline(L, fake, K, Fout, n=256, seconds=10.0, warmup=10, min_passes=50):
     """The oracle (tests-only CPU restatement: scipy SpMM in the reference's
     order + numpy/BLAS GEMMs and layout transposes, fp32) timed on the SAME
-    workload as the GPU line -- config B, batch 256, fwd+bwd -- for a bounded
-    number of repetitions (>= 1, until ~`seconds`), BLAS on every CPU this
-    process may use (the scipy SpMM itself is single-threaded, as TF's CPU
-    SparseTensorDenseMatMul functor the survey describes)."""
+    workload as the GPU line -- config B, batch 256, fwd+bwd -- as §8d says:
+    the median of >= 50 timed passes after 10 warm-up passes, BLAS on every
+    CPU this process may use (the scipy SpMM itself is single-threaded, as TF's
+    CPU SparseTensorDenseMatMul functor the survey describes)."""
     from threadpoolctl import threadpool_limits
     from oracle import cheb_oracle as O
     from cnn_graph_amd.graph import rescale_L, canonical_csr
@@ -126,23 +142,112 @@ def cpu_baseline(L, fake, K, Fout, n=256, seconds=10.0):
     x[:, fake, :] = 0
     W = (rng.standard_normal((K, Fout)) * 0.1).astype(np.float32)
     dy = rng.standard_normal((n, M, Fout)).astype(np.float32)
+
+    def one_pass():
+        basis, _y = O.cheb_forward(x, rp, ci, v, W, K, dtype=np.float32)
+        O.cheb_backward(dy, basis, W, rp, ci, v, n, M, 1, K, dtype=np.float32)
+
     with threadpool_limits(limits=threads):
-        t0 = time.perf_counter()
-        reps = 0
-        while True:
-            basis, _y = O.cheb_forward(x, rp, ci, v, W, K, dtype=np.float32)
-            O.cheb_backward(dy, basis, W, rp, ci, v, n, M, 1, K, dtype=np.float32)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el > seconds:
-                break
+        times = cpu_pass_times(one_pass, warmup, min_passes, seconds)
+    med = float(np.median(times))
     q = "none" if quota is None else f"{quota:g}"
-    return {"value": round(reps * n / el, 1), "unit": "samples/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": f"{reps} fwd+bwd passes of the full config-B batch (N={n}, M={M}, K={K}, "
-                      f"Fout={Fout}; oracle/cheb_oracle.py, fp32) in {el:.1f}s; BLAS threads = "
-                      f"{threads} = the CPUs this process may use (affinity {aff}, cgroup quota {q}; "
-                      f"os.cpu_count() = {ncpu} is the whole machine); scipy SpMM single-threaded"}
+    return {"value": round(n / med, 1), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "pass_ms_median": round(med * 1e3, 2),
+            "pass_ms_p90": round(float(np.percentile(times, 90)) * 1e3, 2),
+            "sample": f"median of {len(times)} timed fwd+bwd passes (after {warmup} warm-up) of the "
+                      f"full config-B batch (N={n}, M={M}, K={K}, Fout={Fout}; oracle/cheb_oracle.py, "
+                      f"fp32); BLAS threads = {threads} = the CPUs this process may use (affinity "
+                      f"{aff}, cgroup quota {q}; os.cpu_count() = {ncpu} is the whole machine); "
+                      f"scipy SpMM single-threaded"}
+
+
+def _cpu_leg(name, fn, n, n_full, what, warmup, min_passes, seconds, per_sample=True):
+    """Time `fn` (one fwd+bwd pass over n samples of config `name`) on the host
+    cores by cpu_pass_times; samples/s from the median pass.  n < n_full: a
+    stated sub-batch of the config's per-GPU batch (the oracle's cost is linear
+    in the batch: every sample is filtered independently)."""
+    from threadpoolctl import threadpool_limits
+    threads, aff, quota, ncpu = host_cpus()
+    with threadpool_limits(limits=threads):
+        times = cpu_pass_times(fn, warmup, min_passes, seconds)
+    med = float(np.median(times))
+    q = "none" if quota is None else f"{quota:g}"
+    exc = "" if len(times) >= 50 and warmup >= 10 else (
+        f" (exception to §8d's >= 50 after 10: {len(times)} passes after {warmup} warm-up, bounded "
+        f"to ~{seconds:g} s of CPU work per config)")
+    sub = "" if n == n_full else f" on a sub-batch of {n} of the config's {n_full} samples per GPU"
+    return {"value": round(n / med, 2), "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "pass_ms_median": round(med * 1e3, 2),
+            "sample": f"config {name}: median of {len(times)} timed fwd+bwd passes{sub}; {what}; BLAS "
+                      f"threads = {threads} (affinity {aff}, cgroup quota {q}; os.cpu_count() = {ncpu})"
+                      + exc}
+
+
+def cpu_baseline_filter(name, Lt, n, n_full, Fin, K, Fout, seconds=10.0, warmup=10, min_passes=50):
+    """chebyshev5 fwd+bwd of configs C1 / C2 / D on the oracle (fp32, the
+    reference's operation order: lib/graph.py:241-258, lib/graph_conv.py:155-176)."""
+    from oracle import cheb_oracle as O
+    from cnn_graph_amd.graph import canonical_csr
+    rp, ci, v = canonical_csr(Lt)
+    M = Lt.shape[0]
+    rng = np.random.default_rng(1)
+    x = rng.random((n, M, Fin), dtype=np.float32)
+    W = (rng.standard_normal((Fin * K, Fout)) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((n, M, Fout)).astype(np.float32)
+
+    def one_pass():
+        basis, _y = O.cheb_forward(x, rp, ci, v, W, K, dtype=np.float32)
+        O.cheb_backward(dy, basis, W, rp, ci, v, n, M, Fin, K, dtype=np.float32)
+
+    return _cpu_leg(name, one_pass, n, n_full,
+                    f"oracle/cheb_oracle.py fp32, M={M}, nnz={len(ci)}, Fin={Fin}, K={K}, Fout={Fout}",
+                    warmup, min_passes, seconds)
+
+
+def cpu_baseline_lstm(Lt, n, n_full, T, Fin, H, K, seconds=10.0, warmup=2, min_passes=50):
+    """Config E: one gconv-LSTM layer's T-step forward + BPTT on the oracle
+    (float64 restatement of lib/gconv_lstm.py:77-221 under static_rnn)."""
+    from oracle import lstm_oracle as LO
+    from cnn_graph_amd.graph import canonical_csr
+    rp, ci, v = canonical_csr(Lt)
+    lap = (rp, ci, v.astype(np.float64))
+    M = Lt.shape[0]
+    rng = np.random.default_rng(2)
+    xs = rng.random((T, n, M, Fin))
+    p = [rng.uniform(-0.1, 0.1, (K * Fin, 4 * H)), rng.uniform(-0.1, 0.1, (K * H, 4 * H)),
+         rng.uniform(-0.3, 0.3, 4 * H)]
+    gh = rng.standard_normal((T, n, M, H))
+
+    def one_pass():
+        _, _, caches = LO.layer_forward(xs, p, lap, K, H)
+        LO.layer_backward(gh, None, caches, p, lap, K, H)
+
+    return _cpu_leg("E", one_pass, n, n_full,
+                    f"oracle/lstm_oracle.py float64, T={T}, M={M}, Fin={Fin}, H={H}, K={K}",
+                    warmup, min_passes, seconds)
+
+
+def cpu_baseline_resgnn(L, n, n_full, Fin, F, K, R, seconds=10.0, warmup=2, min_passes=50):
+    """Config R: one ResGNN training step (forward, MSE, backward, Adam) on the
+    oracle (float64 restatement of lib/graph_conv.py:305-330 + lib/graph_model.py:246-310)."""
+    from oracle import model_oracle as MO
+    from cnn_graph_amd.graph import canonical_csr, rescale_L
+    rp, ci, v = canonical_csr(rescale_L(L, 2))
+    lap = (rp, ci, v.astype(np.float64))
+    M = L.shape[0]
+    rng = np.random.default_rng(3)
+    x = rng.random((n, M, Fin))
+    labels = rng.random((n, M, 2))
+    Ws = [rng.standard_normal((fi * K, fo)) * 0.1
+          for fi, fo in [(Fin, F)] + [(F, F)] * (2 * R) + [(F, 2)]]
+    state = [(np.zeros_like(w), np.zeros_like(w)) for w in Ws]
+
+    def one_pass():
+        MO.train_step(x, labels, Ws, lap, K, R, state, 1, 1e-3)
+
+    return _cpu_leg("R", one_pass, n, n_full,
+                    f"oracle/model_oracle.py float64, M={M}, Fin={Fin}, nfilter={F}, K={K}, "
+                    f"{R} residual layers", warmup, min_passes, seconds)
 
 
 def burst_ms(fn, reps=50, rounds=5):
@@ -275,21 +380,13 @@ def main():
     W = truncated_normal_(torch.empty((Fin * K, Fout), device=dev), 0.1)
     cdist.broadcast_parameters([W])
     dy = torch.randn((N, M, Fout), device=dev, generator=g)
-    m_adam = torch.zeros_like(W)
-    v_adam = torch.zeros_like(W)
 
-    # basis layout: rows by default (the orders layout's faster forward is
-    # outweighed by its slower fused-dW backward on config B: DESIGN.md §5)
     runner = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=args.basis_layout)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    adam = _lib.lib().cg_adam_update
-    adam_args = (W.data_ptr(), runner.dW.data_ptr(), m_adam.data_ptr(), v_adam.data_ptr(),
-                 W.numel(), ctypes.c_float(1e-3), ctypes.c_float(0.9), ctypes.c_float(0.999),
-                 ctypes.c_float(1e-8))
-    scale = ctypes.c_float(1.0 / world)
     exchange = world > 1 or args.force_allreduce
     comm = None
     rccl_nranks = None
+    allreduce = None
     if exchange and args.allreduce == "rccl":
         comm = cdist.RcclComm(local)
         ar_fn = _lib.lib().cg_allreduce_sum_f32
@@ -299,46 +396,27 @@ def main():
         if rccl_nranks != world:
             sys.exit(f"bench.py: RCCL communicator spans {rccl_nranks} ranks, expected {world}")
 
-    # No exchange step (one GPU): the Adam update rides on the dW reduction
-    # (cg_cheb_backward_adam) instead of a separate launch.  With an exchange
-    # (N > 1), the update of the all-reduced dW is applied by the NEXT step's
-    # forward (cg_cheb_forward_adam: W, m, v double-buffered, no Adam launch);
-    # step i's forward applies step i-1's gradient, so every timed step still
-    # does one forward, backward, all-reduce and Adam update.
-    fuse_adam = not exchange and not args.unfused_adam
-    fwd_adam = exchange and not args.unfused_adam
-    Wb = [W, torch.empty_like(W)]
-    mb = [m_adam, torch.zeros_like(W)]
-    vb = [v_adam, torch.zeros_like(W)]
+        def allreduce(s):
+            st = ar_fn(*ar_args, s)
+            if st:
+                _lib.check("cg_allreduce_sum_f32", st)
+    elif exchange:
+        def allreduce(s):
+            dist.all_reduce(runner.dW, op=dist.ReduceOp.SUM)
+
+    # The step schedule (cnn_graph_amd/dp_step.py, driven at world 2 by
+    # tests/test_gpu_dp_bench.py): with no exchange step (one GPU) the Adam
+    # update rides on the dW reduction (cg_cheb_backward_adam) instead of a
+    # separate launch; with an exchange (N > 1) the update of the all-reduced dW
+    # is applied by the NEXT step's forward (cg_cheb_forward_adam: W, m, v
+    # double-buffered, no Adam launch), so every timed step is one forward,
+    # backward, all-reduce and Adam update.
+    trainer = ChebTrainStep(runner, x, dy, W, world=world, allreduce=allreduce,
+                            schedule="unfused" if args.unfused_adam else "auto")
+    fuse_adam, fwd_adam = trainer.schedule == "fused", trainer.schedule == "forward"
 
     def step(i, stream=stream):
-        if fwd_adam:
-            if i == 0:
-                runner.forward(x, Wb[0], stream=stream)
-            else:
-                pi, ci = (i - 1) % 2, i % 2
-                runner.forward_adam(x, Wb[pi], runner.dW, mb[pi], vb[pi], Wb[ci], mb[ci], vb[ci],
-                                    i, grad_scale=1.0 / world, stream=stream)
-            Wc = Wb[i % 2]
-        else:
-            Wc = W
-            runner.forward(x, W, stream=stream)
-        if fuse_adam:
-            runner.backward_adam(dy, W, m_adam, v_adam, i + 1, grad_scale=1.0 / world,
-                                 stream=stream)
-            return
-        runner.backward(dy, Wc, stream=stream)
-        if exchange:
-            if comm is not None:
-                st = ar_fn(*ar_args, stream)
-                if st:
-                    _lib.check("cg_allreduce_sum_f32", st)
-            else:
-                dist.all_reduce(runner.dW, op=dist.ReduceOp.SUM)
-        if not fwd_adam:
-            st = adam(*adam_args, i + 1, scale, stream)
-            if st:
-                _lib.check("cg_adam_update", st)
+        trainer.step(i, stream)
 
     # HIP graph of the K timed steps (captured untimed, after the warmup): the
     # timed region is one replay, so the host's per-launch cost (ctypes + the
@@ -461,7 +539,8 @@ def main():
         "data": "synthetic (x~U[0,1) with fake vertices 0, dy~N(0,1), W~truncnorm(0,0.1)); "
                 "graph = reference MNIST recipe M=976",
         "config": {"workload": "config B: MNIST 8-NN grid coarsened, M=976, nnz=6396, K=25, Fin=1, "
-                               "Fout=32, chebyshev5 fwd+bwd + dW all-reduce + Adam",
+                               "Fout=32, chebyshev5 fwd+bwd" + (" + dW all-reduce" if exchange else "")
+                               + " + Adam",
                    "batch_per_gpu": N, "global_batch": N_global, "M": M, "nnz": plan.nnz, "K": K,
                    "Fin": Fin, "Fout": Fout, "path": path, "basis_layout": runner.basis_layout,
                    "parallelism": f"dp{world}",

@@ -113,6 +113,7 @@ _SIGNATURES = {
     "cg_lstm_seq_forward": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp,
                              _vp, _vp, _vp, _vp, _c_i64, _vp, _c_sz, _vp], _c_int),
     "cg_lstm_seq_status": ([_vp, _c_i32, _vp, ctypes.POINTER(_c_i32), _vp], _c_int),
+    "cg_lstm_seq_fault": ([_vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32)], _c_int),
     "cg_lstm_seq_x_supported": ([_vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i32)], _c_int),
     "cg_lstm_seq_forward_x": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp,
                                _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _c_sz,

@@ -58,6 +58,14 @@ struct cg_plan {
     bool ok = false;  // max row length <= cg::kFastWidth and M <= 1024
     long gather_cycles = 0, gather_ideal = 0;  // modelled LDS cycles per step
   } fast, tfast;
+  // the gconv-LSTM sequence launches' sticky fault word: host-mapped pinned
+  // memory the kernel writes (system scope) when a pair hand-off times out,
+  // read by cg_lstm_seq_fault without a device copy once seq_event (recorded
+  // behind every sequence launch) has completed
+  int* seq_fault = nullptr;      // host pointer
+  int* seq_fault_dev = nullptr;  // its device alias
+  hipEvent_t seq_event = nullptr;
+  bool seq_launched = false;
 };
 
 namespace {
@@ -273,6 +281,8 @@ void free_plan(cg_plan* p) {
   if (p->tslots.buf) (void)hipFree(p->tslots.buf);
   if (p->fast.buf) (void)hipFree(p->fast.buf);
   if (p->tfast.buf) (void)hipFree(p->tfast.buf);
+  if (p->seq_event) (void)hipEventDestroy(p->seq_event);
+  if (p->seq_fault) (void)hipHostFree(p->seq_fault);
   delete p;
 }
 
@@ -1524,7 +1534,7 @@ int cg_lstm_seq_x_supported(const cg_plan* plan, int32_t Fin, int32_t H, int32_t
 
 int cg_lstm_seq_workspace_bytes(const cg_plan* plan, int32_t N, size_t* bytes) {
   if (!plan || !bytes || N < 1) return fail(CG_ERR_ARG, "lstm_seq_workspace_bytes: bad arguments");
-  *bytes = al256(sizeof(int) * (size_t(2) * cg::lstm_seq_pairs(N, plan->device) + 1));
+  *bytes = al256(sizeof(int) * size_t(2) * cg::lstm_seq_pairs(N, plan->device));
   return ok();
 }
 
@@ -1570,10 +1580,27 @@ static int lstm_seq_impl(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t
   if ((rc = check_device(plan))) return rc;
   const int P = cg::lstm_seq_pairs(N, plan->device);
   int* flags = static_cast<int*>(workspace);
+  if (!plan->seq_fault) {
+    void* hp = nullptr;
+    CG_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    plan->seq_fault = static_cast<int*>(hp);
+    *plan->seq_fault = 0;
+    void* dp = nullptr;
+    CG_HIP(hipHostGetDevicePointer(&dp, hp, 0));
+    plan->seq_fault_dev = static_cast<int*>(dp);
+    CG_HIP(hipEventCreateWithFlags(&plan->seq_event, hipEventDisableTiming));
+  }
+  // fault injection for the tests (a pair whose workgroup 0 stops publishing
+  // from step CG_SEQ_INJECT_HANG on): read at every launch
+  const char* inj = getenv("CG_SEQ_INJECT_HANG");
+  const int inject_t = (inj && inj[0]) ? atoi(inj) : -1;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   CG_HIP(cg::launch_lstm_seq(gates, T, N, plan->M, K, plan->nnz, plan->rowptr, plan->col, plan->val,
                              plan->lorder, xs, Wx, Fin, xplanes, xplane_stride, gx, Wh, bias, h0,
-                             c0, hs, cs, act, planes, plane_stride, flags, flags + 2 * P, P,
-                             reinterpret_cast<hipStream_t>(stream)));
+                             c0, hs, cs, act, planes, plane_stride, flags, plan->seq_fault_dev, P, s,
+                             inject_t));
+  CG_HIP(hipEventRecord(plan->seq_event, s));
+  plan->seq_launched = true;
   return ok();
 }
 
@@ -1596,18 +1623,35 @@ int cg_lstm_seq_forward_x(cg_plan* plan, int32_t T, int32_t N, int32_t Fin, int3
                        bias, h0, c0, hs, cs, act, planes, plane_stride, workspace, ws_bytes, stream);
 }
 
+int cg_lstm_seq_fault(cg_plan* plan, int32_t wait, int32_t clear, int32_t* fault) {
+  if (!plan || !fault) return fail(CG_ERR_ARG, "lstm_seq_fault: null argument");
+  *fault = 0;
+  if (!plan->seq_launched) return ok();
+  if (wait) {
+    CG_HIP(hipEventSynchronize(plan->seq_event));
+  } else {
+    const hipError_t q = hipEventQuery(plan->seq_event);
+    if (q == hipErrorNotReady) {
+      *fault = -1;  // the last sequence launch is still in flight
+      return ok();
+    }
+    if (q != hipSuccess) return fail(CG_ERR_HIP, "lstm_seq_fault: %s", hipGetErrorString(q));
+  }
+  const int v = __atomic_load_n(plan->seq_fault, __ATOMIC_ACQUIRE);
+  if (!v) return ok();
+  *fault = 1;
+  if (clear) __atomic_store_n(plan->seq_fault, 0, __ATOMIC_RELEASE);
+  return fail(CG_ERR_HIP, "lstm_seq_forward: a workgroup pair hand-off timed out (a partner "
+                          "workgroup was not co-resident); the launch's hs / cs / act hold NaN "
+                          "from the lost step on");
+}
+
 int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,
                        void* stream) {
-  if (!plan || !workspace || !status || N < 1) return fail(CG_ERR_ARG, "lstm_seq_status: bad arguments");
-  const int P = cg::lstm_seq_pairs(N, plan->device);
-  int v = 0;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  CG_HIP(hipMemcpyAsync(&v, static_cast<const int*>(workspace) + 2 * P, sizeof(int),
-                        hipMemcpyDeviceToHost, s));
-  CG_HIP(hipStreamSynchronize(s));
-  *status = v;
-  if (v) return fail(CG_ERR_HIP, "lstm_seq_forward: a workgroup pair hand-off timed out");
-  return ok();
+  if (!plan || !status || N < 1) return fail(CG_ERR_ARG, "lstm_seq_status: bad arguments");
+  (void)workspace;  // the fault word lives in the plan (sticky), not in the workspace
+  CG_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+  return cg_lstm_seq_fault(const_cast<cg_plan*>(plan), 1, 0, status);
 }
 
 int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,

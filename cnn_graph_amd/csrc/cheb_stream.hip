@@ -585,7 +585,7 @@ __global__ __launch_bounds__(64 * NW) void k_dw_slabs(const float* __restrict__ 
                                                   float* __restrict__ slab, int pl_fin,
                                                   int64_t pl_stride, int K, int tpb,
                                                   const float* __restrict__ xb, int x_fin,
-                                                  int64_t x_stride, int FinKh) {
+                                                  int64_t x_stride, int FinKh, int ldd) {
   typedef typename std::conditional<VW == 4, float4, float>::type V;
   constexpr int kDwNB = dw_nb<VW>();
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(64 * NW) void k_dw_slabs(const float* __restrict__ 
         if (av[i]) ra[q][i] = rv ? *reinterpret_cast<const V*>(basis + rr * ald + aoff[i]) : V{};
 #pragma unroll
       for (int i = 0; i < kDwNB; ++i)
-        if (bv[i]) rbv[q][i] = rv ? *reinterpret_cast<const V*>(dy + rr * Fout + VW * (lane + 64 * i)) : V{};
+        if (bv[i]) rbv[q][i] = rv ? *reinterpret_cast<const V*>(dy + rr * ldd + VW * (lane + 64 * i)) : V{};
     }
   };
   auto stage = [&]() {
@@ -703,7 +703,7 @@ __global__ __launch_bounds__(64 * NW) void k_dw_slabs(const float* __restrict__ 
       const int jx = jj - FinKh;
       const int jo = jj >= FinKh ? (jx < nxc ? FinKh + (jx % x_fin) * K + jx / x_fin : jj)
                                  : pl_fin > 0 ? (jj % pl_fin) * K + jj / pl_fin : jj;
-      if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jo) * Fout + ff] = acc[a][r];
+      if (jj < FinK && ff < Fout) slab[(int64_t(blockIdx.x) * FinK + jo) * ldd + ff] = acc[a][r];
     }
   }
 }
@@ -906,17 +906,21 @@ int dw_chunks(int64_t R) {
   return int(c < 1 ? 1 : c);
 }
 
-hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
-                           float* slab, hipStream_t s, int pl_fin, int64_t pl_stride, int K,
-                           const float* xb, int x_fin, int64_t x_stride) {
+static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int64_t R, int FinKh,
+                                       int Fout, int ldd, float* slab, hipStream_t s, int pl_fin,
+                                       int64_t pl_stride, int K, const float* xb, int x_fin,
+                                       int64_t x_stride) {
   const int chunks = dw_chunks(R);
   const int64_t rpc = (R + chunks - 1) / chunks;
-  if (xb && (x_fin < 1 || x_fin * K + 1 > 64)) return hipErrorInvalidValue;
   const int FinK = FinKh + (xb ? x_fin * K + 1 : 0);
   const int jtl = (FinK + 31) / 32, ftl = (Fout + 31) / 32;
   const int ntiles = jtl * ftl;
-  const int vw = (FinKh % 4 == 0 && Fout % 4 == 0 && (pl_fin == 0 || pl_fin % 4 == 0)) ? 4 : 1;
-  if (Fout > 256) return hipErrorInvalidValue;
+  // float4 pieces only where every piece is a whole aligned float4: column
+  // counts, row strides, plane stride and both base pointers
+  const bool a16 = (reinterpret_cast<uintptr_t>(basis) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(dy) & 15) == 0;
+  const int vw = (a16 && FinKh % 4 == 0 && Fout % 4 == 0 && ldd % 4 == 0 &&
+                  (pl_fin == 0 || (pl_fin % 4 == 0 && pl_stride % 4 == 0))) ? 4 : 1;
   // tiles per block: as many as the staging pieces allow (every group
   // re-reads the chunk's dy rows and its own basis columns)
   int tpb = kDwTiles, groups = 0, span = 0;
@@ -942,17 +946,33 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
   }();
   if (vw == 4 && nw == 8)
     hipLaunchKernelGGL((k_dw_slabs<4, 8>), grid, dim3(512), lds, s, basis, dy, R, FinK, Fout, rpc,
-                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh, ldd);
   else if (vw == 4)
     hipLaunchKernelGGL((k_dw_slabs<4, 4>), grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
-                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh, ldd);
   else if (nw == 8)
     hipLaunchKernelGGL((k_dw_slabs<1, 8>), grid, dim3(512), lds, s, basis, dy, R, FinK, Fout, rpc,
-                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh, ldd);
   else
     hipLaunchKernelGGL((k_dw_slabs<1, 4>), grid, dim3(256), lds, s, basis, dy, R, FinK, Fout, rpc,
-                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh);
+                       slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh, ldd);
   return hipGetLastError();
+}
+
+hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
+                           float* slab, hipStream_t s, int pl_fin, int64_t pl_stride, int K,
+                           const float* xb, int x_fin, int64_t x_stride) {
+  if (xb && (x_fin < 1 || x_fin * K + 1 > 64)) return hipErrorInvalidValue;
+  // the kernel stages at most 256 dy columns per row: wider outputs run as
+  // column slices of 256 (each slice its own launch over the same rows, slab
+  // columns f0 .. f0 + 255 of the same [chunk][FinK][Fout] slabs)
+  for (int f0 = 0; f0 < Fout; f0 += 256) {
+    const int fw = Fout - f0 < 256 ? Fout - f0 : 256;
+    const hipError_t e = launch_dw_slabs_cols(basis, dy + f0, R, FinKh, fw, Fout, slab + f0, s,
+                                              pl_fin, pl_stride, K, xb, x_fin, x_stride);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,

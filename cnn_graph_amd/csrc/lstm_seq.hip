@@ -28,7 +28,9 @@
 //   (write-through) stores, each wave drains (s_waitcnt vmcnt(0)), the
 //   workgroup barrier, then ONE lane stores the step counter sc1 into the
 //   pair's flag; the partner polls it (sc1 loads, s_sleep, bounded by a
-//   wall-clock timeout that sets a status word and ends the launch), joins a
+//   wall-clock timeout: a workgroup that times out writes NaN into every hs /
+//   cs / act entry it still owed -- its units of this and every later step and
+//   sample -- sets the plan's sticky fault word and ends), joins a
 //   barrier, and reads the other half of h with sc1 loads
 //   (MI355X_MICROARCH.md §inter-workgroup visibility, table row 1).  A
 //   workgroup does its OWN two quarters first, so the partner's half has
@@ -148,7 +150,8 @@ struct SeqArgs {
   float* planes;      // T_k of h_{t-1} at (k-1)*pstride + [T][N][M][32], or NULL
   int64_t pstride;
   int* flags;         // [P][2] step counters (zeroed before the launch)
-  int* status;        // [1] 0 = ok, 1 = a hand-off timed out
+  int* status;        // the plan's sticky fault word (host-mapped): set to 1 when a hand-off
+                      // times out, never cleared by a launch
   unsigned long long timeout;  // wall-clock ticks
   int dbg;            // ablation build only (CG_DBG): 1 no MFMA, 2 no SpMM, 4 no gate math,
                       // 8 no partner wait, 16 no gx / c loads, 32 no plane stores,
@@ -156,7 +159,28 @@ struct SeqArgs {
   unsigned long long* ts;  // ablation build: phase stamps of step 1 (CG_TS), else NULL
   int xpre;           // 1: xplanes already hold T_k(x_t) for every step (launch_lstm_seq's
                       // pre-pass): the x contraction reads them, no x recurrence in the loop
+  int inject_t;       // fault injection (CG_SEQ_INJECT_HANG, tests only): >= 0 makes workgroup
+                      // 0 of pair 0 stop publishing its step counter from that step on
 };
+
+// A timed-out workgroup's outputs: NaN in every hs / cs / act entry of its
+// units [16u, 16u + 16) from step t0 of sample n0 on, and every step of the
+// pair's later samples, so nothing downstream can consume unwritten memory
+__device__ void lstm_seq_poison(const SeqArgs& A, int n0, int t0, int u) {
+  const float qnan = __builtin_nanf("");
+  const int M = A.M;
+  for (int n = n0; n < A.N; n += A.P)
+    for (int t = (n == n0 ? t0 : 0); t < A.T; ++t) {
+      const int64_t rb = (int64_t(t) * A.N + n) * M;
+      for (int e = threadIdx.x; e < M * 16; e += kST) {
+        const int64_t o = (rb + (e >> 4)) * kH + 16 * u + (e & 15);
+        A.hs[o] = qnan;
+        A.cs[o] = qnan;
+      }
+      if (A.act)
+        for (int e = threadIdx.x; e < M * 64; e += kST) A.act[(rb + (e >> 6)) * 128 + 64 * u + (e & 63)] = qnan;
+    }
+}
 
 template <bool XPRE>
 __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
@@ -418,7 +442,8 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
       // quarters above) and the own quarters' planes of step t
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(my_flag, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0 && !(A.inject_t >= 0 && pair == 0 && u == 0 && base + t >= A.inject_t))
+        __hip_atomic_store(my_flag, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (has_h) {
         if (!CG_DBG(A.dbg, 8)) {
           // the partner's quarters of step t: wait for its counter
@@ -430,13 +455,16 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
               __builtin_amdgcn_s_sleep(1);
               if (wall_clock64() - t0 > A.timeout) {
                 s_abort = 1;
-                __hip_atomic_store(A.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(A.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
               }
             }
           }
           __syncthreads();
-          if (s_abort) return;  // every thread of the workgroup returns here
+          if (s_abort) {  // every thread of the workgroup: poison what it owed, end
+            lstm_seq_poison(A, n, t, u);
+            return;
+          }
         }
         if (stamp) CG_TS(A.ts, 2);
         // the partner's two quarters: T_0 = its half of h_{t-1}, T_k its planes
@@ -795,7 +823,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
                            const float* Wx, int Fin, float* xplanes, int64_t xpstride, const float* gx, const float* Wh,
                            const float* bias, const float* h0, const float* c0, float* hs,
                            float* cs, float* act, float* planes, int64_t pstride, int* flags,
-                           int* status, int P, hipStream_t s) {
+                           int* status, int P, hipStream_t s, int inject_t) {
   if (!lstm_seq_ok(M, kH, K, nnz, xs ? Fin : 0) || N < 1 || T < 1 || P < 1 || P > N ||
       (xs && (Fin < 1 || Fin > 8 || !Wx || !xplanes)) || (!xs && !gx))
     return hipErrorInvalidValue;
@@ -809,7 +837,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   if (attr0 != hipSuccess) return attr0;
   if (attr1 != hipSuccess) return attr1;
   int dev = 0, rate_khz = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
       rate_khz <= 0)
     rate_khz = 100000;  // 100 MHz
@@ -817,11 +845,11 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
             P % 8 == 0 ? 1 : 0, gx, xs, Wx, xplanes, xpstride, Fin, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
             // a pair hand-off that has not happened after 2 s ends the launch
             static_cast<unsigned long long>(rate_khz) * 2000ull, (debug_flags() >> 16) & 0xff,
-            nullptr, 0};
+            nullptr, 0, inject_t};
 #ifdef CG_DEBUG
   a.ts = g_debug_ts;
 #endif
-  hipError_t e = hipMemsetAsync(flags, 0, sizeof(int) * (size_t(2) * P + 1), s);
+  hipError_t e = hipMemsetAsync(flags, 0, sizeof(int) * size_t(2) * P, s);
   if (e != hipSuccess) return e;
   // x basis of all T steps up front (plane 0 = x, plane k = T_k(x) by the
   // streaming steps over the T*N samples: CSR order from +0, the same values
@@ -842,8 +870,11 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   }
   // a pair waits for its partner, so every workgroup of the grid must be
   // resident at once: check the grid against the occupancy query (what a
-  // cooperative launch would check, MI355X_MICROARCH.md §Residency), with one
-  // workgroup per CU of margin, then launch plainly
+  // cooperative launch would check, MI355X_MICROARCH.md §Residency; the LDS
+  // footprint admits one workgroup per CU, so the grid is at most one per CU)
+  // and launch plainly.  Residency on an idle chip is all this buys: kernels of
+  // other streams or processes can hold CUs, which is what the hand-off
+  // timeout, the NaN poisoning and the plan's fault word are for
   const size_t lds = lstm_seq_lds(M, K, nnz, xs ? Fin : 0);
   int per_cu = 0, cus = 0;
   const void* kern = a.xpre ? reinterpret_cast<const void*>(&k_lstm_seq<true>)

@@ -230,7 +230,8 @@ class _Layer(torch.autograd.Function):
     T h-convs, BPTT with one weight-gradient GEMM for the h-weights)."""
 
     @staticmethod
-    def forward(ctx, xs, c0, h0, Wx, Wh, b, cell: GConvLSTMCell, zero_init: bool):
+    def forward(ctx, xs, c0, h0, Wx, Wh, b, cell: GConvLSTMCell, zero_init: bool,
+                check_now: bool):
         H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
         xs = xs.contiguous()
         T, N, M, F = xs.shape
@@ -253,6 +254,8 @@ class _Layer(torch.autograd.Function):
         basis_h = None if fused else torch.empty((T, R, H * K), **f32)
         gh = None if fused else torch.empty((N, M, 4 * H), **f32)
         if cell.seq:
+            # a hand-off fault of an earlier launch on this plan not reported yet
+            ops.lstm_seq_fault(plan, wait=False)
             # all T steps in one launch.  The h basis of every step as K planes
             # [K][T+1][R][H] of one buffer: plane 0 at t = h_{t-1} (hs IS
             # plane 0 shifted by one step, slot 0 = h0), planes k >= 1 written
@@ -275,6 +278,11 @@ class _Layer(torch.autograd.Function):
                                      c0=None if zero_init else c0, out_hs=hs, out_cs=cs,
                                      out_act=act, planes=hp[1] if K > 1 else None,
                                      plane_stride=(T + 1) * R * H)
+            # a lost pair hand-off leaves NaN in hs / cs / act: an inference call
+            # checks the launch before returning its outputs, a training call
+            # before its backward consumes them (one event wait, no device sync)
+            if check_now:
+                ops.lstm_seq_fault(plan, wait=True)
         for t in range(0 if cell.seq else T):
             h_prev = (None if zero_init else h0) if t == 0 else hs[t - 1]
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
@@ -297,6 +305,8 @@ class _Layer(torch.autograd.Function):
         basis_x, hb, Wx, Wh, act, cs, c0, h0, hs = ctx.saved_tensors
         cell, zero_init, fused = ctx.cell, ctx.zero_init, ctx.fused
         H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
+        if cell.seq:  # raises CGError if the forward's launch lost a pair hand-off
+            ops.lstm_seq_fault(plan, wait=True)
         T, N, M, F = ctx.shape
         R = N * M
         dev = act.device
@@ -337,7 +347,7 @@ class _Layer(torch.autograd.Function):
                                            need_dW=False)
             dx_out = dxs.view(T, N, M, F) if dxs is not None else None
             return (dx_out, None if zero_init else dc, None if zero_init else dh_rec, dWx, dWh, db,
-                    None, None)
+                    None, None, None)
         if T <= t_first:
             dWh = torch.zeros_like(Wh)
         elif cell.seq:  # one GEMM over the K planes of every step with an h-conv
@@ -361,19 +371,26 @@ class _Layer(torch.autograd.Function):
         dx_out = dxs.view(T, N, M, F) if dxs is not None else None
         dc0 = None if zero_init else dc
         dh0 = None if zero_init else dh_rec
-        return dx_out, dc0, dh0, dWx, dWh, db, None, None
+        return dx_out, dc0, dh0, dWx, dWh, db, None, None, None
 
 
 def layer(cell: GConvLSTMCell, xs: torch.Tensor, initial_state=None):
     """Run ``cell`` over xs [T, N, M, feat_in]; returns (hs [T, N, M, H],
-    LSTMStateTuple(c_T, h_T)).  initial_state None = zero state."""
+    LSTMStateTuple(c_T, h_T)).  initial_state None = zero state.
+
+    On the one-launch path a lost pair hand-off (cg_lstm_seq_fault) raises
+    CGError: here when no gradient will be taken (the outputs go straight to
+    the caller), else at the start of the backward, before any gradient is
+    formed from them (the outputs then hold NaN from the lost step on)."""
+    ins = [xs, cell.Wx, cell.Wh, cell.b] + ([] if initial_state is None else list(initial_state))
+    check_now = not (torch.is_grad_enabled() and any(t.requires_grad for t in ins))
     if initial_state is None:
         z = xs.new_zeros(())
-        hs, cT = _Layer.apply(xs, z, z, cell.Wx, cell.Wh, cell.b, cell, True)
+        hs, cT = _Layer.apply(xs, z, z, cell.Wx, cell.Wh, cell.b, cell, True, check_now)
     else:
         c0, h0 = initial_state
         hs, cT = _Layer.apply(xs, c0.contiguous(), h0.contiguous(), cell.Wx, cell.Wh, cell.b, cell,
-                              False)
+                              False, check_now)
     return hs, LSTMStateTuple(cT, hs[-1])
 
 

@@ -644,6 +644,17 @@ def lstm_seq_supported(plan: ChebPlan, H: int, K: int) -> bool:
     return bool(ok.value)
 
 
+def lstm_seq_fault(plan: ChebPlan, wait: bool = True) -> bool | None:
+    """The plan's sticky sequence-launch fault word (cg_lstm_seq_fault): raises
+    CGError (and resets the word) if a pair hand-off of any k_lstm_seq launch
+    so far timed out -- that launch's hs / cs / act then hold NaN from the lost
+    step on.  wait=True blocks until the last launch has completed and returns
+    False; wait=False never blocks and returns None while it is in flight."""
+    f = ctypes.c_int32()
+    _lib.call("cg_lstm_seq_fault", plan.handle, int(bool(wait)), 1, ctypes.byref(f))
+    return None if f.value < 0 else False
+
+
 def lstm_seq_forward(plan: ChebPlan, gx, Wh, bias, K: int, T: int, N: int, gates="reference",
                      h0=None, c0=None, out_hs=None, out_cs=None, out_act=None, planes=None,
                      plane_stride: int = 0, check: bool = False):
@@ -651,7 +662,8 @@ def lstm_seq_forward(plan: ChebPlan, gx, Wh, bias, K: int, T: int, N: int, gates
     gx [T, N, M, 4H] (the x-conv of every step), h0 / c0 [N, M, H] or None
     (zero state).  planes (optional; a tensor whose storage holds K-1 planes
     [T, N, M, H] plane_stride floats apart) receives T_k of h_{t-1}, k >= 1.
-    check=True waits for the stream and raises if a pair hand-off timed out.
+    check=True waits for the launch and raises CGError if a pair hand-off timed
+    out (lstm_seq_fault); without it the fault surfaces at the next check.
     Returns (hs [T, N, M, H], cs [T, N, M, H], act or None) -- act UNIT-major,
     [T, N, M, 4H] holding act[..., 4u + g] (g = z, i, f, o): lstm_bwd_step
     reads it with act_unit_major=True."""
@@ -694,8 +706,7 @@ def lstm_seq_forward(plan: ChebPlan, gx, Wh, bias, K: int, T: int, N: int, gates
               _p(gx), _p(Wh), _p(bias), _p(h0), _p(c0), _p(hs), _p(cs), _p(out_act), _p(planes),
               int(plane_stride), _p(ws), int(nb.value), s)
     if check:
-        st = ctypes.c_int32()
-        _lib.call("cg_lstm_seq_status", plan.handle, int(N), _p(ws), ctypes.byref(st), s)
+        lstm_seq_fault(plan, wait=True)
     return hs, cs, out_act
 
 
@@ -737,6 +748,13 @@ def lstm_seq_forward_x(plan: ChebPlan, xs, Wx, Wh, bias, K: int, gates="referenc
     if planes is None and K > 1:
         planes = torch.empty((K - 1, R, H), **f32)
         plane_stride = R * H
+    if planes is not None:
+        _check_dev("planes", planes)
+        need = (K - 2) * plane_stride + R * H if K > 1 else 0
+        avail = planes.untyped_storage().nbytes() // 4 - planes.storage_offset()
+        if K > 1 and (plane_stride < R * H or avail < need or planes.data_ptr() % 16
+                      or plane_stride % 4):
+            raise ValueError("planes: storage too small / misaligned for the K-1 planes")
     if xplanes is None:
         xplanes = torch.empty((K, R, F), **f32)
     _check_out("xplanes", xplanes, (K * R * F,))
@@ -748,8 +766,7 @@ def lstm_seq_forward_x(plan: ChebPlan, xs, Wx, Wh, bias, K: int, gates="referenc
               _p(xs), _p(Wx), _p(xplanes), R * F, _p(Wh), _p(bias), _p(h0), _p(c0), _p(hs), _p(cs),
               _p(out_act), _p(planes), int(plane_stride), _p(ws), int(nb.value), s)
     if check:
-        st = ctypes.c_int32()
-        _lib.call("cg_lstm_seq_status", plan.handle, int(N), _p(ws), ctypes.byref(st), s)
+        lstm_seq_fault(plan, wait=True)
     return hs, cs, out_act, xplanes
 
 

@@ -355,9 +355,17 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
  *   k = 1..K-1 at (k-1)*plane_stride + [T][N][M][H] (steps with an h-conv
  *   only; each workgroup computes the orders of its own 16 channels and reads
  *   its partner's from here)
- *   workspace: cg_lstm_seq_workspace_bytes (step counters + a status word).
- * cg_lstm_seq_status: waits for the stream, returns CG_ERR_HIP if a pair
- *   hand-off timed out (the launch then ends early instead of hanging).
+ *   workspace: cg_lstm_seq_workspace_bytes (the pairs' step counters).
+ *   A pair hand-off that times out (a partner workgroup not co-resident, e.g.
+ *   CUs held by another stream's kernel) ends the launch instead of hanging:
+ *   the lost workgroups write NaN into every hs / cs / act entry they still
+ *   owed and set the plan's STICKY fault word.
+ * cg_lstm_seq_fault: the plan's fault word over every sequence launch so far.
+ *   wait = 1 blocks until the last launch has completed; wait = 0 never blocks
+ *   and reports *fault = -1 while it is still in flight.  *fault = 1 (and
+ *   CG_ERR_HIP) when a hand-off timed out; clear = 1 then resets the word.
+ * cg_lstm_seq_status: (compatibility) synchronises the stream, then
+ *   cg_lstm_seq_fault(plan, 1, 0, status); the workspace is not read.
  * cg_lstm_bwd_step: one BPTT step in ONE launch: dpre (the gradient of the
  *   gate pre-activations, [N][M][4H]), dc_prev and dh_prev = the h-conv's
  *   input gradient (reverse Chebyshev recurrence over L~^T of dpre Wh^T).
@@ -382,6 +390,7 @@ int cg_lstm_seq_forward_x(cg_plan* plan, int32_t T, int32_t N, int32_t Fin, int3
                           const float* h0, const float* c0, float* hs, float* cs, float* act,
                           float* planes, int64_t plane_stride, void* workspace, size_t ws_bytes,
                           void* stream);
+int cg_lstm_seq_fault(cg_plan* plan, int32_t wait, int32_t clear, int32_t* fault);
 int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,
                        void* stream);
 int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,

@@ -9,8 +9,12 @@
 
 fwd / bwd are HIP-event timings (torch's current stream, where every C-ABI
 call is enqueued) of one chebyshev5 forward and backward (dx + dW), median of
-rounds; alg_GBps uses SURVEY.md §8d's algorithmic bytes.
+rounds; alg_GBps uses SURVEY.md §8d's algorithmic bytes.  Each line carries a
+`cpu_baseline`: the oracle's fwd+bwd of the same config on the host cores
+(bench.py's CPU legs -- the only place outside tests/ that runs oracle/),
+median of the timed passes, with the sub-batch and pass count stated.
 Usage: python scripts/bench_configs.py [C1 C2 D E R] [--d-batch N] [--layout rows|planes]
+                                       [--no-cpu] [--cpu-seconds S]
 """
 from __future__ import annotations
 
@@ -27,6 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
+import bench  # noqa: E402  (the CPU legs)
 from cnn_graph_amd import ops  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
@@ -77,6 +82,14 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="rows")
             "samples_per_s": round(N / ((f + b) * 1e-3), 1),
             "fwd_alg_GBps": round(bf / (f * 1e-3) / 1e9, 1),
             "bwd_alg_GBps": round(bb / (b * 1e-3) / 1e9, 1)}
+
+
+def graph_e():
+    """config E's grid graph: (L~, L = L~ + I so that rescale_L(L, 2) = L~)."""
+    with np.load(os.path.join(ROOT, "tests", "golden", "golden_E.npz"), allow_pickle=False) as z:
+        M = int(z["M"])
+        Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
+    return Lt, (Lt + scipy.sparse.identity(M, dtype=np.float32, format="csr")).tocsr()
 
 
 def lstm_config(dev, T=12, N=128, Fin=2, H=32, K=3, hconv="auto"):
@@ -143,6 +156,8 @@ def main():
     ap.add_argument("--layout", default="rows", choices=["rows", "planes"],
                     help="basis layout of the C1/C2/D filters (planes: where it applies)")
     ap.add_argument("--rounds", type=int, default=3, help="timed rounds per measurement (median)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
     global ROUNDS
     ROUNDS = args.rounds
@@ -150,27 +165,42 @@ def main():
     torch.cuda.set_device(dev)
     from cnn_graph_amd.graph import rescale_L
     for name in args.configs:
+        cpu = None
         if name in ("C1", "C2"):
             with np.load(os.path.join(ROOT, "tests", "golden", "golden_C.npz"), allow_pickle=False) as z:
                 M = int(z["M"])
                 Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
             Fin = 1 if name == "C1" else 32
             out = filter_config(name, Lt, 128, Fin, 5, 32, dev, args.variant, args.layout)
+            # the oracle's C2 pass is ~27 s at N = 128: a sub-batch of 8
+            nc = 128 if name == "C1" else 8
+            cpu = lambda: bench.cpu_baseline_filter(name, Lt, nc, 128, Fin, 5, 32,  # noqa: E731
+                                                    seconds=args.cpu_seconds,
+                                                    warmup=10 if nc == 128 else 2)
         elif name == "D":
             import synth_graphs
             Lt = rescale_L(synth_graphs.config_d_laplacian(), 2)
             out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev, args.variant, args.layout)
+            cpu = lambda: bench.cpu_baseline_filter("D", Lt, 1, args.d_batch, 64, 3, 64,  # noqa: E731
+                                                    seconds=args.cpu_seconds, warmup=1,
+                                                    min_passes=3)
         elif name == "E":
             out = lstm_config(dev)
+            cpu = lambda: bench.cpu_baseline_lstm(graph_e()[0], 8, 128, 12, 2, 32, 3,  # noqa: E731
+                                                  seconds=args.cpu_seconds)
         elif name == "E_unfused":
             out = lstm_config(dev, hconv="unfused")
         elif name == "E_step":
             out = lstm_config(dev, hconv="fused")
         elif name == "R":
             out = resgnn_config(dev)
+            cpu = lambda: bench.cpu_baseline_resgnn(graph_e()[1], 2, 100, 2, 32, 20, 4,  # noqa: E731
+                                                    seconds=args.cpu_seconds)
         else:
             raise SystemExit(f"unknown config {name}")
         if out is not None:
+            if not args.no_cpu and cpu is not None:
+                out["cpu_baseline"] = cpu()
             print(json.dumps(out), flush=True)
 
 

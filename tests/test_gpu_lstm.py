@@ -404,3 +404,49 @@ def test_lstm_weight_grads_one_pass(dev, Fin, K):
         ref = torch.einsum("krc,rg->ckg", pl, d64).reshape(w * K, 4 * H)
         assert O.normwise_err(got.cpu().numpy(), ref.numpy()) < 1e-5
     assert O.normwise_err(db.cpu().numpy(), d64.sum(0).numpy()) < 1e-5
+
+
+def test_seq_handoff_timeout_raises_and_poisons(dev, monkeypatch):
+    """A lost pair hand-off (fault injected: workgroup 0 of pair 0 stops
+    publishing its step counter from step 1, CG_SEQ_INJECT_HANG=1) ends the
+    launch after the 2 s timeout instead of hanging, and no caller can consume
+    its outputs: every hs / cs entry the lost workgroups owed is NaN, an
+    inference layer() raises CGError, a training layer()'s backward raises
+    before forming any gradient, and the plan works again afterwards."""
+    from cnn_graph_amd import _lib, ops
+    from cnn_graph_amd.gconv_lstm import layer
+    Lt, _, M = graph_E()
+    T, N, Fin, H, K = 3, 4, 2, 32, 3
+    cell, _ = make_cell(Lt, Fin, H, K, "reference", dev, seed=61)
+    assert cell.seq
+    g = torch.Generator(device=dev)
+    g.manual_seed(9)
+    xs = torch.rand((T, N, M, Fin), device=dev, generator=g)
+    with torch.no_grad():
+        ref, _ = layer(cell, xs)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(ref).all())
+    monkeypatch.setenv("CG_SEQ_INJECT_HANG", "1")
+    with torch.no_grad():
+        with pytest.raises(_lib.CGError, match="hand-off timed out"):
+            layer(cell, xs)
+    # the explicit call: the poisoned entries.  Pair 0 (sample 0): workgroup 1
+    # (units 16..31) times out at step 1, workgroup 0 (units 0..15) at step 2
+    hs, cs, _, _ = ops.lstm_seq_forward_x(cell.plan, xs, cell.Wx.detach(), cell.Wh.detach(),
+                                          cell.b.detach(), K, "reference")
+    with pytest.raises(_lib.CGError):
+        ops.lstm_seq_fault(cell.plan, wait=True)
+    for a in (hs, cs):
+        assert bool(torch.isnan(a[1, 0, :, 16:]).all()) and bool(torch.isnan(a[2, 0]).all())
+        assert bool(torch.isfinite(a[0]).all()) and bool(torch.isfinite(a[:, 1:]).all())
+        assert bool(torch.isfinite(a[1, 0, :, :16]).all())
+    assert torch.equal(hs[:, 1:], ref[:, 1:])
+    # training: the forward returns, its backward refuses
+    hs2, _ = layer(cell, xs)
+    with pytest.raises(_lib.CGError, match="hand-off timed out"):
+        hs2.sum().backward()
+    monkeypatch.delenv("CG_SEQ_INJECT_HANG")
+    assert ops.lstm_seq_fault(cell.plan, wait=True) is False  # reported once, then reset
+    with torch.no_grad():
+        again, _ = layer(cell, xs)
+    assert torch.equal(again, ref)

@@ -139,12 +139,12 @@ def test_resgnn_humanflow_shape_train_steps_vs_oracle(dev):
     # updated weights are ill-conditioned in the gradients' rounding at K = 20:
     # the oracle recomputes loss and gradients from the GPU's weights of each
     # step, and the update is checked as the oracle's Adam of the GPU gradient
-    # The gradients compose ten K = 20 filters (each output within the 1e-5
-    # filter bar, test_gpu_parity / test_gpu_basis_layout) through the ReLUs
-    # and residual adds.  Contracting in 16- instead of 8-channel groups moves
-    # a hidden layer's y by 7.8e-7 (basis, dx, dW bitwise equal:
-    # scripts/grp16_check.py) and these gradients by up to 3.4e-5 against the
-    # float64 oracle, so they get 5e-5
+    # The gradients compose ten K = 20 filters through the ReLUs and residual
+    # adds; every filter alone is held to 1e-5 on the GPU's own inputs by
+    # test_resgnn_humanflow_shape_per_filter_vs_oracle, which also shows that
+    # what separates this end-to-end comparison from 1e-5 is ReLU-mask flips
+    # between the float64 chain and the GPU's (the float64 chain's backward
+    # through the GPU's masks is within 1e-5), so the chain gets 5e-5
     GTOL = 5e-5
     state = [(np.zeros_like(f64(w)), np.zeros_like(f64(w))) for w in model.W]
     for step in range(1, 4):
@@ -162,6 +162,111 @@ def test_resgnn_humanflow_shape_train_steps_vs_oracle(dev):
             new_state.append((m2, v2))
             assert O.normwise_err(f64(w), rw) < TOL, (step, name)
         state = new_state
+
+
+def _filter_inputs(net, x):
+    """(input, residual) of every filter of a _ResNet as the GPU ran it: the
+    trainer's own saved outputs (lib/graph_conv.py:305-330 wiring)."""
+    ins, res = [x], [None]
+    h, li = net.out[0], 1
+    for _ in range(net.o.R):
+        ins += [h, net.out[li]]
+        res += [None, h]
+        h, li = net.out[li + 1], li + 2
+    ins.append(h)
+    res.append(None)
+    return ins, res
+
+
+def test_resgnn_humanflow_shape_per_filter_vs_oracle(dev):
+    """Config R's shape (K = 20, nfilter 32, nres_layer_count 4, Fin 2, config
+    E's 1024-vertex graph, hidden layers on the planes layout with the 16-
+    channel group forward k_grp16_fwd and the fused-dBasis backward
+    k_grp_clen_dy): EVERY filter of three optimizer steps at the 1e-5 bar,
+    each on the inputs, residuals and upstream gradients the GPU itself
+    produced (as test_gpu_large::test_config_c_two_layers_chained_full_batch
+    does): y = act(cheb(x) W + res), dW and dx (accumulated where the schedule
+    accumulates) against float64.
+
+    The end-to-end comparison (every gradient against a float64 chain run from
+    x alone) is the secondary check below, at 5e-5: a float64 chain's ReLU
+    masks differ from the GPU's wherever a pre-activation sits within fp32
+    rounding of 0, and one flipped mask entry passes (or drops) a whole
+    upstream-gradient entry.  The test counts those flips and shows they carry
+    the difference: the float64 chain's backward taken with the GPU's masks is
+    back within 1e-5 of the GPU's gradients."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.model import ResGNN
+    L, _ = golden_L("golden_E.npz")
+    N, K, F, R, Fin = 3, 20, 32, 4, 2
+    model = ResGNN(L, N=N, Fin=Fin, nfilter=F, K=K, nres_layer_count=R, learning_rate=1e-3,
+                   decay_rate=0.95, decay_steps=2, device=dev, seed=13)
+    assert ops.basis_layout_for(model.plan, N, F, K, F) == "planes"
+    net = model.net
+    lap = (model.plan.rowptr, model.plan.col, model.plan.val.astype(np.float64))
+    M = model.M
+    rng = np.random.default_rng(17)
+    x = rng.random((N, M, Fin)).astype(np.float32)
+    labels = rng.random((N, M, 2)).astype(np.float32)
+    calls = []
+    run_b = net._b
+
+    def recording_b(li, dy, dz, dx, dx_acc, s):  # the schedule's own calls, snapshotted
+        before = dx.clone() if (dx is not None and dx_acc) else None
+        dy_in = dy.clone()
+        run_b(li, dy, dz, dx, dx_acc, s)
+        calls.append((li, dy_in, None if dx is None else dx.clone(), before, net.dW[li].clone()))
+
+    net._b = recording_b
+    xt = t(x, dev)
+    flips_total = 0
+    for step in range(1, 4):
+        Wprev = [f64(w) for w in model.W]
+        calls.clear()
+        loss = model.train_step(xt, t(labels, dev))
+        torch.cuda.synchronize()
+        ins, res = _filter_inputs(net, xt)
+        As, gpu_mask = [], []
+        for li, (name, fi, fo, act) in enumerate(net.layers):
+            A, y = cheb_conv64(f64(ins[li]), lap, Wprev[li], K)
+            pre = y + f64(res[li]) if res[li] is not None else y
+            ref = np.maximum(pre, 0) if act == "relu" else pre
+            err = O.normwise_err(f64(net.out[li]), ref)
+            assert err < TOL, (step, name, "y", err)
+            As.append(A)
+            gpu_mask.append(f64(net.out[li]) > 0 if act == "relu" else None)
+        assert len(calls) == len(net.layers)
+        for li, dy, dx, before, dW in calls:
+            name, fi, fo, act = net.layers[li]
+            dz = f64(dy) * gpu_mask[li] if act == "relu" else f64(dy)
+            rdx, rdW = O.cheb_backward(dz, As[li], Wprev[li], lap[0], lap[1], lap[2], N, M, fi, K)
+            err = O.normwise_err(f64(dW), rdW)
+            assert err < TOL, (step, name, "dW", err)
+            if dx is not None:
+                ref_dx = rdx + (f64(before) if before is not None else 0.0)
+                err = O.normwise_err(f64(dx), ref_dx)
+                assert err < TOL, (step, name, "dx", err)
+        # secondary: the float64 chain from x alone
+        out64, cache = MO.forward(x.astype(np.float64), Wprev, lap, K, R)
+        rl, dout64 = MO.loss_and_grad(out64, labels)
+        assert abs(float(loss.item()) - rl) <= 1e-5 * rl, (step, float(loss.item()), rl)
+        flips = [int(np.count_nonzero((c[2] > 0) != m)) if m is not None else 0
+                 for c, m in zip(cache, gpu_mask)]
+        flips_total += sum(flips)
+        rdW = MO.backward(dout64, cache, Wprev, lap, K, R)
+        e2e = [O.normwise_err(f64(g), r) for g, r in zip(model.dW, rdW)]
+        assert max(e2e) < 5e-5, (step, e2e, flips)
+        # the same float64 chain, backward through the GPU's ReLU masks
+        masked = [(inp, A, np.where(m, np.maximum(o, 1e-300), 0.0) if m is not None else o, a)
+                  for (inp, A, o, a), m in zip(cache, gpu_mask)]
+        rdW_m = MO.backward(dout64, masked, Wprev, lap, K, R)
+        e2e_m = [O.normwise_err(f64(g), r) for g, r in zip(model.dW, rdW_m)]
+        assert max(e2e_m) < TOL, (step, e2e_m, flips)
+        if max(e2e) >= TOL:  # then the masks carried it
+            assert sum(flips) > 0, (step, e2e, flips)
+        print(f"step {step}: ReLU mask flips per filter {flips}; end-to-end dW err "
+              f"max {max(e2e):.2e}, with the GPU's masks {max(e2e_m):.2e}")
+    net._b = run_b
 
 
 def test_graphconv_residual_network_autograd_matches_trainer(dev):
