@@ -708,6 +708,123 @@ __global__ __launch_bounds__(64 * NW) void k_dw_slabs(const float* __restrict__ 
   }
 }
 
+// ---- dW on registers only: k_dw_direct -----------------------------------
+// The slabs of k_dw_slabs, bitwise -- the same chunks, the same row pairs in
+// the same order for every output element, the same v_mfma_f32_32x32x2_f32 --
+// without LDS or barriers: each wave owns one chunk and NA x NB output tiles of
+// it (a column group grp of the basis, all of dy) and streams the chunk's rows
+// straight from HBM into the MFMA operand registers, PD row pairs in flight.
+// Lane (i, h) of an MFMA needs column i of row r + h of each operand; a
+// V-float load gives a lane V consecutive columns V*i .. V*i + V-1 of one row,
+// i.e. its operand for V "virtual tiles" (tile e holds the columns V*i + e):
+// a permutation of where an output element sits in the accumulators, not of
+// the products summed into it.  For large row counts (config D: 65 536 rows
+// per chunk) this replaces k_dw_slabs' 16-row LDS batches and their two
+// barriers per batch.
+struct DwDirectArgs {
+  const float* basis;
+  const float* dy;
+  int64_t R, rpc;
+  int chunks, G;         // chunks x column groups = waves
+  int FinKh, Fout, ldd;  // basis columns, dy columns (this slice), dy / slab row stride
+  float* slab;
+  int pl_fin;            // > 0: planes layout (column jj = k*pl_fin + fin)
+  int64_t pl_stride;
+  int K;
+};
+
+template <int V> struct DwVec { typedef float T; };
+template <> struct DwVec<2> { typedef float2 T; };
+template <> struct DwVec<4> { typedef float4 T; };
+template <int V> __device__ __forceinline__ float dw_el(const typename DwVec<V>::T& v, int e) {
+  return reinterpret_cast<const float*>(&v)[e];
+}
+
+template <int VA, int NLA, int VB, int NLB, int PD>
+__global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
+  typedef typename DwVec<VA>::T TA;
+  typedef typename DwVec<VB>::T TB;
+  constexpr int NA = VA * NLA, NB = VB * NLB;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int gw = blockIdx.x * 4 + w;
+  const int chunk = gw / A.G, grp = gw - chunk * A.G;
+  if (chunk >= A.chunks) return;
+  const int64_t c0 = int64_t(chunk) * A.rpc;
+  const int64_t c1 = (c0 + A.rpc < A.R) ? c0 + A.rpc : A.R;
+  const int cg0 = grp * 32 * NA;  // the group's first basis column
+  const int64_t ald = A.pl_fin > 0 ? A.pl_fin : A.FinKh;
+  const float* pa[NLA];
+  bool av[NLA];
+#pragma unroll
+  for (int q = 0; q < NLA; ++q) {
+    const int c = cg0 + 32 * VA * q + VA * li;
+    av[q] = c < A.FinKh;
+    const int64_t off = A.pl_fin > 0 ? int64_t(c / A.pl_fin) * A.pl_stride + c % A.pl_fin : c;
+    pa[q] = A.basis + (av[q] ? off : 0) + (c0 + h) * ald;
+  }
+  const float* pb[NLB];
+  bool bv[NLB];
+#pragma unroll
+  for (int q = 0; q < NLB; ++q) {
+    const int f = 32 * VB * q + VB * li;
+    bv[q] = f < A.Fout;
+    pb[q] = A.dy + (bv[q] ? f : 0) + (c0 + h) * int64_t(A.ldd);
+  }
+  const int64_t npairs = (c1 - c0 + 1) >> 1;
+  TA ra[PD][NLA];
+  TB rb[PD][NLB];
+  auto fetch = [&](int s, int64_t p) {  // row pair p into ring slot s (zeros past the chunk)
+    const bool rv = c0 + 2 * p + h < c1;
+    const int64_t oa = 2 * p * ald, ob = 2 * p * int64_t(A.ldd);
+#pragma unroll
+    for (int q = 0; q < NLA; ++q) ra[s][q] = (rv && av[q]) ? *reinterpret_cast<const TA*>(pa[q] + oa) : TA{};
+#pragma unroll
+    for (int q = 0; q < NLB; ++q) rb[s][q] = (rv && bv[q]) ? *reinterpret_cast<const TB*>(pb[q] + ob) : TB{};
+  };
+  f32x16 acc[NA][NB];
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < PD; ++s) fetch(s, s);
+  for (int64_t p0 = 0; p0 < npairs; p0 += PD) {
+#pragma unroll
+    for (int s = 0; s < PD; ++s) {
+      if (p0 + s < npairs) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          const float x = dw_el<VA>(ra[s][a / VA], a % VA);
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, dw_el<VB>(rb[s][b / VB], b % VB),
+                                                             acc[a][b], 0, 0, 0);
+        }
+        if (p0 + s + PD < npairs) fetch(s, p0 + s + PD);
+      }
+    }
+  }
+  // tile (a, b), accumulator r: A lane i = (r & 3) + 8 (r >> 2) + 4 h, B lane li
+  const int FinK = A.FinKh;
+#pragma unroll
+  for (int a = 0; a < NA; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int f = 32 * VB * (b / VB) + VB * li + b % VB;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int c = cg0 + 32 * VA * (a / VA) + VA * i + a % VA;
+        const int jo = A.pl_fin > 0 ? (c % A.pl_fin) * A.K + c / A.pl_fin : c;
+        if (c < A.FinKh && f < A.Fout)
+          A.slab[(int64_t(chunk) * FinK + jo) * A.ldd + f] = acc[a][b][r];
+      }
+    }
+}
+
 // out[i] = sum_z slab[z][i] in a FIXED order (bitwise reproducible): wave w of
 // a block sums the slabs z = w, w+16, ... for 64 consecutive outputs (one
 // 256-B coalesced load per slab, 8 in flight), then the 16 partial sums are
@@ -906,12 +1023,48 @@ int dw_chunks(int64_t R) {
   return int(c < 1 ? 1 : c);
 }
 
+// k_dw_direct for this shape, if one of its instantiations serves it: the dy
+// columns of the slice decide the B loads (VB, NLB), the basis columns are cut
+// into G groups of NA = VA*NLA virtual tiles; CG_DW_DIRECT=0 keeps k_dw_slabs
+// (A/B runs), =2 prefers two-float basis loads (fewer, larger groups)
+static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
+                             int ldd, float* slab, hipStream_t s, int pl_fin, int64_t pl_stride,
+                             int K, int chunks, int64_t rpc, hipError_t* err) {
+  const char* env = getenv("CG_DW_DIRECT");  // read per call: tests switch it in-process
+  const int mode = (env && env[0]) ? atoi(env) : 1;
+  if (mode == 0 || rpc < 256) return false;
+  const bool a8 = (reinterpret_cast<uintptr_t>(basis) & 7) == 0;
+  const bool b8 = (reinterpret_cast<uintptr_t>(dy) & 7) == 0;
+  const bool a2 = a8 && FinKh % 2 == 0 && (pl_fin == 0 || (pl_fin % 2 == 0 && pl_stride % 2 == 0));
+  const bool b2 = b8 && Fout % 2 == 0 && ldd % 2 == 0;
+  DwDirectArgs a{basis, dy, R, rpc, chunks, 1, FinKh, Fout, ldd, slab, pl_fin, pl_stride, K};
+  auto go = [&](auto kern, int na) {
+    a.G = (FinKh + 32 * na - 1) / (32 * na);
+    const int64_t waves = int64_t(chunks) * a.G;
+    hipLaunchKernelGGL(kern, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, s, a);
+    *err = hipGetLastError();
+    return true;
+  };
+  if (Fout <= 32) return go(k_dw_direct<1, 5, 1, 1, 12>, 5);
+  if (!b2) return false;
+  if (Fout <= 64) {
+    if (mode == 2 && a2) return go(k_dw_direct<2, 3, 2, 1, 8>, 6);
+    return go(k_dw_direct<1, 3, 2, 1, 12>, 3);
+  }
+  if (Fout <= 128) return go(k_dw_direct<1, 3, 2, 2, 8>, 3);
+  return go(k_dw_direct<1, 2, 2, 4, 6>, 2);
+}
+
 static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int64_t R, int FinKh,
                                        int Fout, int ldd, float* slab, hipStream_t s, int pl_fin,
                                        int64_t pl_stride, int K, const float* xb, int x_fin,
                                        int64_t x_stride) {
   const int chunks = dw_chunks(R);
   const int64_t rpc = (R + chunks - 1) / chunks;
+  hipError_t derr = hipSuccess;
+  if (!xb && launch_dw_direct(basis, dy, R, FinKh, Fout, ldd, slab, s, pl_fin, pl_stride, K, chunks,
+                              rpc, &derr))
+    return derr;
   const int FinK = FinKh + (xb ? x_fin * K + 1 : 0);
   const int jtl = (FinK + 31) / 32, ftl = (Fout + 31) / 32;
   const int ntiles = jtl * ftl;

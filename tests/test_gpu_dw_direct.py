@@ -1,0 +1,62 @@
+"""k_dw_direct (dW = basis^T dy on registers only, no LDS batches) against
+k_dw_slabs (CG_DW_DIRECT=0): the per-chunk slabs -- and so dW -- bitwise equal
+(same chunks, same row pairs in the same order per output element, same MFMA),
+on the rows and planes layouts, every dy-width instantiation, ragged row
+counts and column tails; and dW within 1e-5 of float64.  Reference: the
+matmul gradient of lib/graph_conv.py:175."""
+import numpy as np
+import pytest
+
+from oracle import cheb_oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(built_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_graph_amd import _lib
+    _lib.lib()
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("R,FK,Fo", [(300001, 160, 32), (200003, 192, 64), (131072, 96, 128),
+                                     (140001, 40, 256), (102400, 640, 32), (150000, 33, 30),
+                                     (99999, 640, 2)])
+def test_dw_direct_rows_bitwise(dev, monkeypatch, R, FK, Fo):
+    from cnn_graph_amd import ops
+    g = torch.Generator(device=dev)
+    g.manual_seed(R + FK + Fo)
+    A = torch.randn((R, FK), device=dev, generator=g)
+    D = torch.randn((R, Fo), device=dev, generator=g)
+    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    old = ops.weight_grad(A, D)
+    monkeypatch.setenv("CG_DW_DIRECT", "1")
+    new = ops.weight_grad(A, D)
+    torch.cuda.synchronize()
+    assert torch.equal(new, old)
+    ref = A.double().T @ D.double()
+    assert O.normwise_err(new.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("R,Fin,K,Fo", [(200001, 64, 3, 64), (102400, 32, 20, 32), (80000, 16, 5, 128)])
+def test_dw_direct_planes_bitwise(dev, monkeypatch, mode, R, Fin, K, Fo):
+    from cnn_graph_amd import ops
+    g = torch.Generator(device=dev)
+    g.manual_seed(R + K)
+    st = R * Fin + 96
+    buf = torch.randn((K * st,), device=dev, generator=g)
+    D = torch.randn((R, Fo), device=dev, generator=g)
+    planes = buf[:R * Fin].view(R, Fin)
+    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    old = ops.weight_grad_planes(planes, st, K, R, D)
+    monkeypatch.setenv("CG_DW_DIRECT", mode)
+    new = ops.weight_grad_planes(planes, st, K, R, D)
+    torch.cuda.synchronize()
+    assert torch.equal(new, old)
+    pl = torch.stack([buf[k * st:k * st + R * Fin].view(R, Fin) for k in range(K)]).double()
+    ref = torch.einsum("krc,rg->ckg", pl, D.double()).reshape(Fin * K, Fo)
+    assert O.normwise_err(new.cpu().numpy(), ref.cpu().numpy()) < 1e-5
