@@ -731,6 +731,12 @@ struct DwDirectArgs {
   int pl_fin;            // > 0: planes layout (column jj = k*pl_fin + fin)
   int64_t pl_stride;
   int K;
+  // the gconv-LSTM's extra columns (VA == 1 only), as k_dw_slabs' xb: x planes
+  // (x column e = plane e / x_fin, fin e % x_fin at xb + plane*x_stride + r*x_fin
+  // + fin, slab column FinKh + fin*K + plane) then one column of ones
+  const float* xb;
+  int x_fin, nxc, FinK;  // nxc = x_fin*K; FinK = FinKh (+ nxc + 1 with xb)
+  int64_t x_stride;
 };
 
 template <int V> struct DwVec { typedef float T; };
@@ -755,13 +761,26 @@ __global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
   const int cg0 = grp * 32 * NA;  // the group's first basis column
   const int64_t ald = A.pl_fin > 0 ? A.pl_fin : A.FinKh;
   const float* pa[NLA];
-  bool av[NLA];
+  int lst[NLA];  // the load's row stride (floats): basis rows or x-plane rows
+  bool av[NLA], aone[NLA];
 #pragma unroll
   for (int q = 0; q < NLA; ++q) {
     const int c = cg0 + 32 * VA * q + VA * li;
     av[q] = c < A.FinKh;
+    aone[q] = false;
     const int64_t off = A.pl_fin > 0 ? int64_t(c / A.pl_fin) * A.pl_stride + c % A.pl_fin : c;
     pa[q] = A.basis + (av[q] ? off : 0) + (c0 + h) * ald;
+    lst[q] = int(ald);
+    if (VA == 1 && A.xb && !av[q]) {
+      const int e = c - A.FinKh;
+      if (e < A.nxc) {
+        av[q] = true;
+        pa[q] = A.xb + int64_t(e / A.x_fin) * A.x_stride + e % A.x_fin + (c0 + h) * A.x_fin;
+        lst[q] = A.x_fin;
+      } else if (e == A.nxc) {
+        aone[q] = true;  // the bias gradient's column of ones
+      }
+    }
   }
   const float* pb[NLB];
   bool bv[NLB];
@@ -776,9 +795,13 @@ __global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
   TB rb[PD][NLB];
   auto fetch = [&](int s, int64_t p) {  // row pair p into ring slot s (zeros past the chunk)
     const bool rv = c0 + 2 * p + h < c1;
-    const int64_t oa = 2 * p * ald, ob = 2 * p * int64_t(A.ldd);
+    const int64_t ob = 2 * p * int64_t(A.ldd);
 #pragma unroll
-    for (int q = 0; q < NLA; ++q) ra[s][q] = (rv && av[q]) ? *reinterpret_cast<const TA*>(pa[q] + oa) : TA{};
+    for (int q = 0; q < NLA; ++q) {
+      ra[s][q] = (rv && av[q]) ? *reinterpret_cast<const TA*>(pa[q] + 2 * p * lst[q]) : TA{};
+      if constexpr (VA == 1)
+        if (aone[q]) ra[s][q] = rv ? 1.f : 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < NLB; ++q) rb[s][q] = (rv && bv[q]) ? *reinterpret_cast<const TB*>(pb[q] + ob) : TB{};
   };
@@ -808,7 +831,7 @@ __global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
     }
   }
   // tile (a, b), accumulator r: A lane i = (r & 3) + 8 (r >> 2) + 4 h, B lane li
-  const int FinK = A.FinKh;
+  const int FinK = A.FinK;
 #pragma unroll
   for (int a = 0; a < NA; ++a)
 #pragma unroll
@@ -818,8 +841,10 @@ __global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
       for (int r = 0; r < 16; ++r) {
         const int i = (r & 3) + 8 * (r >> 2) + 4 * h;
         const int c = cg0 + 32 * VA * (a / VA) + VA * i + a % VA;
-        const int jo = A.pl_fin > 0 ? (c % A.pl_fin) * A.K + c / A.pl_fin : c;
-        if (c < A.FinKh && f < A.Fout)
+        const int jx = c - A.FinKh;
+        const int jo = c >= A.FinKh ? (jx < A.nxc ? A.FinKh + (jx % A.x_fin) * A.K + jx / A.x_fin : c)
+                                    : A.pl_fin > 0 ? (c % A.pl_fin) * A.K + c / A.pl_fin : c;
+        if (c < FinK && f < A.Fout)
           A.slab[(int64_t(chunk) * FinK + jo) * A.ldd + f] = acc[a][b][r];
       }
     }
@@ -1024,34 +1049,43 @@ int dw_chunks(int64_t R) {
 }
 
 // k_dw_direct for this shape, if one of its instantiations serves it: the dy
-// columns of the slice decide the B loads (VB, NLB), the basis columns are cut
-// into G groups of NA = VA*NLA virtual tiles; CG_DW_DIRECT=0 keeps k_dw_slabs
-// (A/B runs), =2 prefers two-float basis loads (fewer, larger groups)
+// columns of the slice decide the B loads (VB, NLB), the basis columns (with
+// the LSTM's x-plane and ones columns) are cut into G groups of NA = VA*NLA
+// virtual tiles, NA chosen for the fewest MFMAs per row pair (G*NA*NB);
+// CG_DW_DIRECT=0 keeps k_dw_slabs (A/B runs), =2 prefers two-float basis loads
 static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
                              int ldd, float* slab, hipStream_t s, int pl_fin, int64_t pl_stride,
-                             int K, int chunks, int64_t rpc, hipError_t* err) {
+                             int K, int chunks, int64_t rpc, const float* xb, int x_fin,
+                             int64_t x_stride, hipError_t* err) {
   const char* env = getenv("CG_DW_DIRECT");  // read per call: tests switch it in-process
   const int mode = (env && env[0]) ? atoi(env) : 1;
   if (mode == 0 || rpc < 256) return false;
   const bool a8 = (reinterpret_cast<uintptr_t>(basis) & 7) == 0;
   const bool b8 = (reinterpret_cast<uintptr_t>(dy) & 7) == 0;
-  const bool a2 = a8 && FinKh % 2 == 0 && (pl_fin == 0 || (pl_fin % 2 == 0 && pl_stride % 2 == 0));
+  const bool a2 = !xb && a8 && FinKh % 2 == 0 && (pl_fin == 0 || (pl_fin % 2 == 0 && pl_stride % 2 == 0));
   const bool b2 = b8 && Fout % 2 == 0 && ldd % 2 == 0;
-  DwDirectArgs a{basis, dy, R, rpc, chunks, 1, FinKh, Fout, ldd, slab, pl_fin, pl_stride, K};
+  const int nxc = xb ? x_fin * K : 0;
+  const int FinK = FinKh + (xb ? nxc + 1 : 0);
+  DwDirectArgs a{basis, dy, R, rpc, chunks, 1, FinKh, Fout, ldd, slab, pl_fin, pl_stride, K,
+                 xb, x_fin > 0 ? x_fin : 1, nxc, FinK, x_stride};
   auto go = [&](auto kern, int na) {
-    a.G = (FinKh + 32 * na - 1) / (32 * na);
+    a.G = (FinK + 32 * na - 1) / (32 * na);
     const int64_t waves = int64_t(chunks) * a.G;
     hipLaunchKernelGGL(kern, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, s, a);
     *err = hipGetLastError();
     return true;
   };
+  auto mfmas = [&](int na) { return (FinK + 32 * na - 1) / (32 * na) * na; };  // per B tile
   if (Fout <= 32) return go(k_dw_direct<1, 5, 1, 1, 12>, 5);
   if (!b2) return false;
   if (Fout <= 64) {
     if (mode == 2 && a2) return go(k_dw_direct<2, 3, 2, 1, 8>, 6);
     return go(k_dw_direct<1, 3, 2, 1, 12>, 3);
   }
-  if (Fout <= 128) return go(k_dw_direct<1, 3, 2, 2, 8>, 3);
+  if (Fout <= 128) {
+    if (mfmas(2) < mfmas(3)) return go(k_dw_direct<1, 2, 2, 2, 10>, 2);
+    return go(k_dw_direct<1, 3, 2, 2, 8>, 3);
+  }
   return go(k_dw_direct<1, 2, 2, 4, 6>, 2);
 }
 
@@ -1062,8 +1096,8 @@ static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int6
   const int chunks = dw_chunks(R);
   const int64_t rpc = (R + chunks - 1) / chunks;
   hipError_t derr = hipSuccess;
-  if (!xb && launch_dw_direct(basis, dy, R, FinKh, Fout, ldd, slab, s, pl_fin, pl_stride, K, chunks,
-                              rpc, &derr))
+  if (launch_dw_direct(basis, dy, R, FinKh, Fout, ldd, slab, s, pl_fin, pl_stride, K, chunks, rpc,
+                       xb, x_fin, x_stride, &derr))
     return derr;
   const int FinK = FinKh + (xb ? x_fin * K + 1 : 0);
   const int jtl = (FinK + 31) / 32, ftl = (Fout + 31) / 32;

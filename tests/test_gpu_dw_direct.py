@@ -60,3 +60,26 @@ def test_dw_direct_planes_bitwise(dev, monkeypatch, mode, R, Fin, K, Fo):
     pl = torch.stack([buf[k * st:k * st + R * Fin].view(R, Fin) for k in range(K)]).double()
     ref = torch.einsum("krc,rg->ckg", pl, D.double()).reshape(Fin * K, Fo)
     assert O.normwise_err(new.cpu().numpy(), ref.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("R,Fin,K", [(12 * 8 * 1024, 2, 3), (50001, 1, 1), (40000, 8, 4)])
+def test_dw_direct_lstm_weight_grads_bitwise(dev, monkeypatch, R, Fin, K):
+    """cg_lstm_weight_grads' one pass (h planes, x planes and the ones column
+    of the bias) on the direct kernel: dWh, dWx, db bitwise k_dw_slabs'."""
+    from cnn_graph_amd import ops
+    H = 32
+    g = torch.Generator(device=dev)
+    g.manual_seed(R + Fin)
+    hst, xst = R * H + 96, R * Fin + 40
+    hbuf = torch.randn((K * hst,), device=dev, generator=g)
+    xbuf = torch.randn((K * xst,), device=dev, generator=g)
+    dpre = torch.randn((R, 4 * H), device=dev, generator=g)
+    hpl, xpl = hbuf[:R * H].view(R, H), xbuf[:R * Fin].view(R, Fin)
+    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    old = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
+    monkeypatch.setenv("CG_DW_DIRECT", "1")
+    new = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
+    torch.cuda.synchronize()
+    for a, b in zip(new, old):
+        assert torch.equal(a, b)
+    assert O.normwise_err(new[2].cpu().numpy(), dpre.double().sum(0).cpu().numpy()) < 1e-5
