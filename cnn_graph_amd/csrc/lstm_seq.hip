@@ -580,6 +580,8 @@ struct BStepArgs {
   float* dpre;          // [N][M][128]
   float* dc_prev;       // [N][M][32] or NULL
   float* dh_prev;       // [N][M][32]
+  int dbg;              // ablation build only: 1 no MFMA, 2 no phase-A loads, 4 no recurrence
+  unsigned long long* ts;  // ablation build: phase stamps (CG_TS), else NULL
 };
 
 template <int K>
@@ -589,6 +591,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int jr = lane & 15, q = lane >> 4;
   const int M = A.M;
+  CG_TS(A.ts, 0);
   int n, u;
   if (A.pair_xcd) {
     const int b = blockIdx.x;
@@ -625,6 +628,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     wl[rt] = wave_max(re[rt] - rb[rt]);
   }
   __syncthreads();
+  CG_TS(A.ts, 1);
   f32x4 acc[kRB][K];
 #pragma unroll
   for (int rt = 0; rt < kRB; ++rt)
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
   for (int rt = 0; rt < kRB; ++rt) {
     const int row = rows[rt];
     float dp[4][8];
-    if (row < M) {
+    if (row < M && !CG_DBG(A.dbg, 2)) {
       const int64_t rr = int64_t(n) * M + row;
       const int64_t hb = rr * kH + 8 * q;
       float av[4][8], cp[8], co[8], dhv[8], dcv[8];
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     }
     // D_o^T[channel 16u + i][row] += Wh_o[.][g] dpre[row][g]
 #pragma unroll
-    for (int o = 0; o < K; ++o) {
+    for (int o = 0; o < K && !CG_DBG(A.dbg, 1); ++o) {
       const float* wo = s_W + o * 2048 + lane;
 #pragma unroll
       for (int s = 0; s < 32; ++s)
@@ -722,6 +726,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
                                                           0, 0, 0);
     }
   }
+  CG_TS(A.ts, 2);
   // phase B: lane (row, q) holds D_o[row][16u + 4q + r] in acc[rt][o][r];
   // G_{k+1} of all rows in the LDS slot, G_{k+2} / G_{k+1} of the lane's own
   // rows in registers; one slot: gather, barrier, overwrite, barrier
@@ -745,7 +750,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     __syncthreads();
   }
 #pragma unroll
-  for (int k = K - 2; k >= 0; --k) {
+  for (int k = K - 2; k >= 0 && !CG_DBG(A.dbg, 4); --k) {
     const float cc = k >= 1 ? 2.f : 1.f;
     float Gn[kRB][4];
 #pragma unroll
@@ -776,12 +781,14 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
       __syncthreads();
     }
   }
+  CG_TS(A.ts, 3);
 #pragma unroll
   for (int rt = 0; rt < kRB; ++rt) {
     if (rows[rt] < M)
       *reinterpret_cast<float4*>(A.dh_prev + (int64_t(n) * M + rows[rt]) * kH + 16 * u + 4 * q) =
           make_float4(G1[rt][0], G1[rt][1], G1[rt][2], G1[rt][3]);
   }
+  CG_TS(A.ts, 4);
 }
 
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
@@ -896,7 +903,11 @@ hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr,
                              float* dh_prev, hipStream_t s) {
   if (!lstm_bstep_ok(M, kH, K, nnzT) || N < 1) return hipErrorInvalidValue;
   BStepArgs a{trowptr, tcol, tval, order, M, round_up(M + 1, 16), N, gates, N % 8 == 0 ? 1 : 0,
-              int(nnzT), act_um ? 1 : 0, dh, dh_rec, dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev};
+              int(nnzT), act_um ? 1 : 0, dh, dh_rec, dc, act, c_prev, c_out, Wh, dpre, dc_prev, dh_prev,
+              (debug_flags() >> 16) & 0xff, nullptr};
+#ifdef CG_DEBUG
+  a.ts = g_debug_ts;
+#endif
   const size_t lds = lstm_bstep_lds(M, K, nnzT);
 #define CG_BSTEP(KK)                                                                              \
   case KK: {                                                                                      \

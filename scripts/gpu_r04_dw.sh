@@ -23,4 +23,6 @@ import json
 for l in open('$O/configs.jsonl'):
     d = json.loads(l); c = d.get('cpu_baseline', {})
     print(d['config'], d.get('fwd_ms'), d.get('bwd_ms', d.get('fwd_bwd_ms', d.get('step_ms'))), d['samples_per_s'], 'cpu', c.get('value'), c.get('pass_ms_median'))"
+timeout -k 10 300 python3 scripts/ablate_bstep.py > $O/ablate_bstep.json 2> $O/ablate_bstep.err || { tail -5 $O/ablate_bstep.err; exit 1; }
+python3 -c "import json; d = json.load(open('$O/ablate_bstep.json')); [print(k, v) for k, v in d.items()]"
 echo DONE
