@@ -266,7 +266,8 @@ struct Fwd {
   template <int L, int CUR, int PRV, int PRV2>
   __device__ __forceinline__ void step(int k) {
 #pragma clang fp contract(off)
-    const V a = r.template dot<FV, L, PRV>(ring);
+    // ablation build: 64 skips the gathers, 128 the own-record writes (LDS attribution)
+    const V a = CG_DBG(A.dbg, 64) ? r.v[0] * t1 : r.template dot<FV, L, PRV>(ring);
     V o;
     if (CG_DBG(A.dbg, 32)) {  // A/B switch: T_{k-2} of the own row re-read from the ring
       const V p = lds_v<FV>(ring + r.rr + PRV2 * 4 * FV);
@@ -274,8 +275,10 @@ struct Fwd {
     } else {           // T_{k-2} of the own row kept in registers (this thread wrote it)
       o = (k == 1) ? a : rec2(a, t2);
     }
-    lds_stv<FV>(ring + r.rb + CUR * 4 * FV, o);
-    lds_stv<FV>(ring + r.rb1 + CUR * 4 * FV, o);
+    if (!CG_DBG(A.dbg, 128)) {
+      lds_stv<FV>(ring + r.rb + CUR * 4 * FV, o);
+      lds_stv<FV>(ring + r.rb1 + CUR * 4 * FV, o);
+    }
     t2 = t1;
     t1 = o;
     __syncthreads();
