@@ -114,6 +114,9 @@ _SIGNATURES = {
                              _vp, _vp, _vp, _vp, _c_i64, _vp, _c_sz, _vp], _c_int),
     "cg_lstm_seq_status": ([_vp, _c_i32, _vp, ctypes.POINTER(_c_i32), _vp], _c_int),
     "cg_lstm_seq_fault": ([_vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32)], _c_int),
+    "cg_dropout_forward": ([_vp, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, _vp, _vp], _c_int),
+    "cg_dropout_backward": ([_vp, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, _vp, _vp], _c_int),
+    "cg_clip_by_norm": ([_vp, ctypes.c_int64, ctypes.c_float, _vp, _vp], _c_int),
     "cg_lstm_seq_x_supported": ([_vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i32)], _c_int),
     "cg_lstm_seq_forward_x": ([_vp, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _c_i32, _vp, _vp, _vp,
                                _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _c_sz,

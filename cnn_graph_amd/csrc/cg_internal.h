@@ -328,6 +328,9 @@ hipError_t launch_slice_channels(const float* x, int64_t rows, int C, int c0, in
                                  hipStream_t s);
 hipError_t launch_stack_merge_fwd(const float* o, const float* w, int N, int64_t MF, int accumulate,
                                   float* y, hipStream_t s);
+hipError_t launch_dropout(const float* x, float* y, int64_t n, float keep, unsigned long long seed,
+                          int bwd, hipStream_t s);
+hipError_t launch_clip_norm(float* t, int64_t n, float c, int* nonfinite, hipStream_t s);
 hipError_t launch_stack_merge_bwd(const float* dy, const float* o, const float* w, int N, int64_t MF,
                                   float* d_o, float* dw, hipStream_t s);
 

@@ -1177,6 +1177,30 @@ int cg_mse_loss_ema(const float* pred, const float* labels, int64_t n, float* lo
   return ok();
 }
 
+int cg_dropout_forward(const float* x, int64_t n, float keep_prob, uint64_t seed, float* y,
+                       void* stream) {
+  if (!x || !y || n < 1 || !(keep_prob > 0.f && keep_prob <= 1.f))
+    return fail(CG_ERR_ARG, "dropout_forward: bad arguments (keep_prob=%g)", keep_prob);
+  CG_HIP(cg::launch_dropout(x, y, n, keep_prob, seed, 0, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_dropout_backward(const float* dy, int64_t n, float keep_prob, uint64_t seed, float* dx,
+                        void* stream) {
+  if (!dy || !dx || n < 1 || !(keep_prob > 0.f && keep_prob <= 1.f))
+    return fail(CG_ERR_ARG, "dropout_backward: bad arguments (keep_prob=%g)", keep_prob);
+  CG_HIP(cg::launch_dropout(dy, dx, n, keep_prob, seed, 1, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_clip_by_norm(float* t, int64_t n, float clip_norm, int32_t* nonfinite, void* stream) {
+  if (!t || n < 1 || !(clip_norm > 0.f))
+    return fail(CG_ERR_ARG, "clip_by_norm: bad arguments (n=%lld, clip_norm=%g)", (long long)n,
+                clip_norm);
+  CG_HIP(cg::launch_clip_norm(t, n, clip_norm, nonfinite, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
 int cg_slice_channels(const float* x, int64_t rows, int32_t C, int32_t c0, int32_t c1, float* out,
                       void* stream) {
   if (!x || !out || rows < 1 || C < 1 || c0 < 0 || c1 <= c0 || c1 > C)

@@ -14,6 +14,14 @@
 //               the stacked-input ResGNN (_inference with stack_num > 1,
 //               lib/graph_conv.py:272-303): channel groups of the input, and
 //               X = sum_i relu(net_i(x_i)) * w_i with w_i [M][F] broadcast over N
+//   k_dropout   DropoutWrapper(output_keep_prob) of glstm_layer
+//               (lib/gconv_lstm.py:616, :623 -> tf.nn.dropout 1.x):
+//               y = (x / keep) * floor(keep + u), u ~ U[0,1) from a counter hash of
+//               (seed, element), so the backward regenerates the same mask:
+//               dx = (dy * floor(keep + u)) / keep (the Mul, then RealDiv gradient)
+//   k_clip_norm tf.clip_by_norm + tf.check_numerics of gconvRNN.Model's
+//               optimizer (lib/gconvRNN.py:392-402): t' = (t * c) / max(||t||, c),
+//               ||t|| from a fixed-order sum of squares, non-finite t' flagged
 // The fast resident forward and the streaming row GEMM apply the residual /
 // ReLU epilogue in their own y store; these kernels are the fallback.
 #include "cg_internal.h"
@@ -34,6 +42,60 @@ __global__ __launch_bounds__(256) void k_act_fwd(float* __restrict__ y, const fl
     if (act) v = v > 0.f ? v : 0.f;
     y[i] = v;
   }
+}
+
+// U[0, 1) of element i under `seed` (splitmix64 finaliser of a Weyl sequence;
+// 24 random bits, so u + keep rounds like tf.random_uniform's fp32 draw)
+__device__ __forceinline__ float drop_u(unsigned long long seed, int64_t i) {
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (static_cast<unsigned long long>(i) + 1ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return float(z >> 40) * (1.f / 16777216.f);
+}
+
+// bwd = 0: y = (x / keep) * floor(keep + u);  bwd = 1: y = (x * floor(keep + u)) / keep
+__global__ __launch_bounds__(256) void k_dropout(const float* __restrict__ x, float* __restrict__ y,
+                                                 int64_t n, float keep, unsigned long long seed,
+                                                 int bwd) {
+#pragma clang fp contract(off)
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    const float b = floorf(keep + drop_u(seed, i));
+    y[i] = bwd ? (x[i] * b) / keep : (x[i] / keep) * b;
+  }
+}
+
+// one workgroup: t <- (t * c) / max(sqrt(sum t^2), c) in place (the norm's sum
+// in a fixed order: lane-strided partials, then a fixed LDS tree), and
+// *nonfinite = 1 when any result is NaN / Inf
+__global__ __launch_bounds__(1024) void k_clip_norm(float* __restrict__ t, int64_t n, float c,
+                                                    int* __restrict__ nonfinite) {
+#pragma clang fp contract(off)
+  __shared__ float part[1024];
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  float s2 = 0.f;
+  for (int64_t i = tid; i < n; i += 1024) s2 = s2 + t[i] * t[i];
+  part[tid] = s2;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if (tid < w) part[tid] = part[tid] + part[tid + w];
+    __syncthreads();
+  }
+  const float l2sum = part[0];
+  // tf.clip_by_norm: l2norm = l2sum > 0 ? sqrt(l2sum) : l2sum
+  const float l2norm = l2sum > 0.f ? sqrtf(l2sum) : l2sum;
+  const float den = l2norm > c ? l2norm : c;
+  int my_bad = 0;
+  for (int64_t i = tid; i < n; i += 1024) {
+    const float v = (t[i] * c) / den;
+    t[i] = v;
+    if (!isfinite(v)) my_bad = 1;
+  }
+  if (my_bad) bad = 1;  // benign race: every writer stores 1
+  __syncthreads();
+  if (tid == 0 && bad && nonfinite) *nonfinite = 1;
 }
 
 __global__ __launch_bounds__(256) void k_relu_bwd(const float* __restrict__ dy,
@@ -251,6 +313,17 @@ hipError_t launch_stack_merge_bwd(const float* dy, const float* o, const float* 
   if (dw)
     hipLaunchKernelGGL(k_stack_merge_dw, dim3(int((MF + 255) / 256)), dim3(256), 0, s, dy, o, N, MF,
                        dw);
+  return hipGetLastError();
+}
+
+hipError_t launch_dropout(const float* x, float* y, int64_t n, float keep, unsigned long long seed,
+                          int bwd, hipStream_t s) {
+  hipLaunchKernelGGL(k_dropout, dim3(grid1d(n, 256)), dim3(256), 0, s, x, y, n, keep, seed, bwd);
+  return hipGetLastError();
+}
+
+hipError_t launch_clip_norm(float* t, int64_t n, float c, int* nonfinite, hipStream_t s) {
+  hipLaunchKernelGGL(k_clip_norm, dim3(1), dim3(1024), 0, s, t, n, c, nonfinite);
   return hipGetLastError();
 }
 

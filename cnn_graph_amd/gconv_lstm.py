@@ -374,14 +374,50 @@ class _Layer(torch.autograd.Function):
         return dx_out, dc0, dh0, dWx, dWh, db, None, None, None
 
 
-def layer(cell: GConvLSTMCell, xs: torch.Tensor, initial_state=None):
+class DropoutWrapper:
+    """tf.nn.rnn_cell.DropoutWrapper(cell, output_keep_prob) as glstm_layer
+    wraps every layer's cell (lib/gconv_lstm.py:616, :623): the cell's OUTPUTS
+    go through tf.nn.dropout (ops.dropout: a HIP kernel, mask regenerated in the
+    backward from a per-call seed), its state passes through untouched.  Like
+    the reference graph, it drops whenever it is applied (there is no training
+    flag); output_keep_prob = 1 is the identity.  The mask stream is seeded
+    from ``seed`` and advances every call (TF's own random stream is not
+    reproducible here, only its semantics)."""
+
+    def __init__(self, cell: GConvLSTMCell, output_keep_prob: float = 1.0, seed: int = 0):
+        if not 0.0 < float(output_keep_prob) <= 1.0:
+            raise ValueError(f"output_keep_prob must be in (0, 1], got {output_keep_prob}")
+        self.cell = cell
+        self.output_keep_prob = float(output_keep_prob)
+        self._seed = int(seed) & ((1 << 64) - 1)
+        self._calls = 0
+
+    def next_seed(self) -> int:
+        self._calls += 1
+        return (self._seed + 0xD1B54A32D192ED03 * self._calls) & ((1 << 64) - 1)
+
+    def __getattr__(self, name):  # state_size, output_size, zero_state, parameters, ...
+        return getattr(self.cell, name)
+
+    def __call__(self, inputs, state, scope=None):
+        out, new_state = self.cell(inputs, state, scope)
+        return ops.dropout(out, self.output_keep_prob, self.next_seed()), new_state
+
+
+def layer(cell, xs: torch.Tensor, initial_state=None):
     """Run ``cell`` over xs [T, N, M, feat_in]; returns (hs [T, N, M, H],
     LSTMStateTuple(c_T, h_T)).  initial_state None = zero state.
 
     On the one-launch path a lost pair hand-off (cg_lstm_seq_fault) raises
     CGError: here when no gradient will be taken (the outputs go straight to
     the caller), else at the start of the backward, before any gradient is
-    formed from them (the outputs then hold NaN from the lost step on)."""
+    formed from them (the outputs then hold NaN from the lost step on).
+
+    ``cell`` may be a DropoutWrapper: the returned outputs are then dropped
+    out, the state (c_T, h_T) is not (DropoutWrapper semantics)."""
+    if isinstance(cell, DropoutWrapper):
+        hs, state = layer(cell.cell, xs, initial_state)
+        return ops.dropout(hs, cell.output_keep_prob, cell.next_seed()), state
     ins = [xs, cell.Wx, cell.Wh, cell.b] + ([] if initial_state is None else list(initial_state))
     check_now = not (torch.is_grad_enabled() and any(t.requires_grad for t in ins))
     if initial_state is None:
@@ -402,7 +438,7 @@ def static_rnn(cells, inputs, initial_states=None):
     states: tuple of LSTMStateTuple per layer).  Layer-by-layer evaluation
     equals the reference's time-major one (layer l at step t depends only on
     layer l-1 at step t and layer l at step t-1)."""
-    if isinstance(cells, GConvLSTMCell):
+    if isinstance(cells, (GConvLSTMCell, DropoutWrapper)):
         cells = [cells]
     xs = torch.stack(list(inputs)) if isinstance(inputs, (list, tuple)) else inputs
     states = []
@@ -411,6 +447,18 @@ def static_rnn(cells, inputs, initial_states=None):
         xs, st = layer(cell, xs, init)
         states.append(st)
     return list(xs.unbind(0)), tuple(states)
+
+
+def clip_gradients(params, max_grad_norm, check_numerics: bool = True):
+    """gconvRNN.Model._build_optim's gradient clipping (lib/gconvRNN.py:392-402)
+    on the parameters' .grad: per variable tf.clip_by_norm(grad, max_grad_norm)
+    then tf.check_numerics (raises FloatingPointError on NaN / Inf), in place
+    on the HIP kernels.  max_grad_norm None = no clipping (the reference's else
+    branch)."""
+    if max_grad_norm is None:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    ops.clip_by_norm_(grads, float(max_grad_norm), check_numerics)
 
 
 def unstack_time(x: torch.Tensor, T: int) -> torch.Tensor:

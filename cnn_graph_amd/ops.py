@@ -809,6 +809,55 @@ def lstm_bwd_step(plan: ChebPlan, dh, dh_rec, dc, act, c_prev, c_out, Wh, K: int
     return dpre, dc_prev, dh_prev
 
 
+class _Dropout(torch.autograd.Function):
+    """tf.nn.dropout (TF 1.x) as DropoutWrapper applies it to a cell's outputs
+    (lib/gconv_lstm.py:616, :623): cg_dropout_forward / cg_dropout_backward,
+    the mask regenerated from ``seed`` in the backward."""
+
+    @staticmethod
+    def forward(ctx, x, keep_prob: float, seed: int):
+        _check_dev("x", x)
+        x = x.contiguous()
+        y = torch.empty_like(x)
+        _lib.call("cg_dropout_forward", _p(x), x.numel(), float(keep_prob), int(seed), _p(y), _stream(x))
+        ctx.keep, ctx.seed = float(keep_prob), int(seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        _lib.call("cg_dropout_backward", _p(dy), dy.numel(), ctx.keep, ctx.seed, _p(dx), _stream(dy))
+        return dx, None, None
+
+
+def dropout(x, keep_prob: float, seed: int):
+    """y = (x / keep_prob) * floor(keep_prob + u), u ~ U[0,1) per element from
+    (seed, index); keep_prob == 1 returns x."""
+    if keep_prob >= 1.0:
+        return x
+    return _Dropout.apply(x, keep_prob, int(seed) & ((1 << 64) - 1))
+
+
+def clip_by_norm_(grads, clip_norm: float, check_numerics: bool = True):
+    """tf.clip_by_norm + tf.check_numerics per gradient tensor, in place
+    (gconvRNN.Model._build_optim, lib/gconvRNN.py:392-402): each g becomes
+    (g * clip_norm) / max(||g||, clip_norm); with check_numerics a NaN / Inf
+    in any clipped gradient raises FloatingPointError (one sync at the end)."""
+    flag = None
+    for g in grads:
+        _check_dev("grad", g)
+        if not g.is_contiguous():
+            raise ValueError("clip_by_norm_: gradients must be contiguous")
+        if flag is None:
+            flag = torch.zeros((1,), device=g.device, dtype=torch.int32)
+        _lib.call("cg_clip_by_norm", _p(g), g.numel(), float(clip_norm),
+                  _p(flag) if check_numerics else None, _stream(g))
+    if check_numerics and flag is not None and int(flag.item()):
+        raise FloatingPointError("Numerical error in gradient (check_numerics after clip_by_norm)")
+    return grads
+
+
 def adam_update(param, grad, m, v, step: int, lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8,
                 grad_scale=1.0):
     """In-place TF-1.x Adam step on device (lib/graph_model.py:293)."""

@@ -399,6 +399,26 @@ int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gat
                      const float* Wh, float* dpre, float* dc_prev, float* dh_prev, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Training-loop pieces of the gconv-LSTM models:
+ * cg_dropout_forward / _backward: tf.nn.rnn_cell.DropoutWrapper(cell,
+ *   output_keep_prob) of glstm_layer (lib/gconv_lstm.py:616, :623), i.e. TF 1.x
+ *   tf.nn.dropout: y = (x / keep) * floor(keep + u), u ~ U[0,1) drawn from a
+ *   counter hash of (seed, element index) -- the backward regenerates the mask
+ *   from the same seed: dx = (dy * floor(keep + u)) / keep.  (TF's random
+ *   stream itself is not reproducible here; the semantics are.)
+ * cg_clip_by_norm: tf.clip_by_norm(t, clip_norm) then tf.check_numerics of
+ *   gconvRNN.Model._build_optim (lib/gconvRNN.py:392-402), in place on one
+ *   gradient tensor: t = (t * clip_norm) / max(||t||_2, clip_norm), the norm a
+ *   fixed-order sum; *nonfinite (device int, nullable) is set to 1 when any
+ *   clipped value is NaN or Inf (the caller raises, as check_numerics does).
+ * ------------------------------------------------------------------------- */
+int cg_dropout_forward(const float* x, int64_t n, float keep_prob, uint64_t seed, float* y,
+                       void* stream);
+int cg_dropout_backward(const float* dy, int64_t n, float keep_prob, uint64_t seed, float* dx,
+                        void* stream);
+int cg_clip_by_norm(float* t, int64_t n, float clip_norm, int32_t* nonfinite, void* stream);
+
+/* ---------------------------------------------------------------------------
  * perm_data (lib/coarsening.py:219-240) on device:
  *   out[n][i][f] = perm[i] < M_in ? x[n][perm[i]][f] : 0   (fake vertices are 0)
  * x [N][M_in][F], perm [M_out] (int32), out [N][M_out][F].

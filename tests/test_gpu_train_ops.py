@@ -1,0 +1,104 @@
+"""Training-loop pieces of the gconv-LSTM models on the HIP kernels:
+DropoutWrapper(output_keep_prob) of glstm_layer (lib/gconv_lstm.py:616, :623;
+tf.nn.dropout 1.x: y = (x / keep) * floor(keep + u)) and gconvRNN.Model's
+tf.clip_by_norm + tf.check_numerics (lib/gconvRNN.py:392-402).  TF's random
+stream is not reproducible here: the dropout tests pin the formula, the mask's
+regeneration in the backward and the keep rate, not TF's draws."""
+import math
+
+import numpy as np
+import pytest
+import scipy.sparse
+
+from conftest import case, load_golden
+from oracle import cheb_oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(built_lib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_graph_amd import _lib
+    _lib.lib()
+    return torch.device("cuda", 0)
+
+
+def test_dropout_formula_mask_and_rate(dev):
+    from cnn_graph_amd import ops
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    n, keep = 1 << 20, 0.8
+    x = torch.randn((n,), device=dev, generator=g)
+    xa = x.clone().requires_grad_()
+    y = ops.dropout(xa, keep, seed=1234)
+    dy = torch.randn((n,), device=dev, generator=g)
+    y.backward(dy)
+    torch.cuda.synchronize()
+    mask = (y != 0)
+    kept = int(mask.sum())
+    # binomial(n, 0.8): 6 sigma
+    assert abs(kept - keep * n) < 6 * math.sqrt(n * keep * (1 - keep))
+    k32 = torch.tensor(keep, dtype=torch.float32)
+    assert torch.equal(y[mask], x[mask] / k32)
+    assert torch.equal(xa.grad, (dy * mask.float()) / k32)
+    # deterministic in the seed, another seed another mask
+    assert torch.equal(ops.dropout(x, keep, 1234), y.detach())
+    assert not torch.equal(ops.dropout(x, keep, 1235) != 0, mask)
+    assert ops.dropout(x, 1.0, 7) is x
+
+
+def test_dropout_wrapper_layer_outputs_only(dev):
+    """DropoutWrapper: outputs dropped, state (c_T, h_T) not; a 2-layer
+    static_rnn feeds the dropped outputs to the next layer."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.gconv_lstm import DropoutWrapper, GConvLSTMCell, layer, static_rnn
+    c = case(load_golden("golden_E.npz"))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    L = (Lt + scipy.sparse.identity(M, dtype=np.float32, format="csr")).tocsr()
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    cell = GConvLSTMCell(32, laplacian=L, lmax=2, K=3, feat_in=2, device=dev, generator=g)
+    xs = torch.rand((4, 2, M, 2), device=dev, generator=g)
+    with torch.no_grad():
+        hs, (cT, hT) = layer(cell, xs)
+        w = DropoutWrapper(cell, 0.8, seed=99)
+        hd, (cT2, hT2) = layer(w, xs)
+        ref = ops.dropout(hs, 0.8, DropoutWrapper(cell, 0.8, seed=99).next_seed())
+    assert torch.equal(hd, ref)
+    assert torch.equal(cT2, cT) and torch.equal(hT2, hT) and torch.equal(hT2, hs[-1])
+    cell2 = GConvLSTMCell(32, laplacian=L, lmax=2, K=3, feat_in=32, device=dev, generator=g)
+    w1, w2 = DropoutWrapper(cell, 0.8, seed=5), DropoutWrapper(cell2, 0.8, seed=6)
+    with torch.no_grad():
+        outs, states = static_rnn([w1, w2], xs)
+        h1, _ = layer(cell, xs)
+        d1 = ops.dropout(h1, 0.8, DropoutWrapper(cell, 0.8, seed=5).next_seed())
+        h2, _ = layer(cell2, d1)
+        d2 = ops.dropout(h2, 0.8, DropoutWrapper(cell2, 0.8, seed=6).next_seed())
+    assert torch.equal(torch.stack(outs), d2)
+    assert torch.equal(states[1].h, h2[-1])
+
+
+def test_clip_by_norm_and_check_numerics(dev):
+    from cnn_graph_amd import ops
+    rng = np.random.default_rng(4)
+    a = rng.standard_normal(5000).astype(np.float32) * 3
+    b = rng.standard_normal((96, 128)).astype(np.float32) * 1e-3
+    ta, tb = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    ops.clip_by_norm_([ta, tb], 5.0)
+    torch.cuda.synchronize()
+    for t, ref in ((ta, a), (tb, b)):
+        r64 = ref.astype(np.float64)
+        nrm = np.sqrt((r64 * r64).sum())
+        assert O.normwise_err(t.cpu().numpy(), r64 * 5.0 / max(nrm, 5.0)) < 1e-6
+    assert torch.equal(tb, torch.from_numpy(b).to(dev) * 5.0 / 5.0)  # norm < 5: unchanged
+    bad = torch.ones((100,), device=dev)
+    bad[17] = float("nan")
+    with pytest.raises(FloatingPointError):
+        ops.clip_by_norm_([ta, bad], 5.0)
+    ok = torch.ones((100,), device=dev)
+    ok[3] = float("inf")
+    ops.clip_by_norm_([ok], 5.0, check_numerics=False)  # no check: no raise
