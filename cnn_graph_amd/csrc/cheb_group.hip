@@ -64,6 +64,7 @@ struct GrpFwdArgs {
   float* basis;     // planes [K][N*M][Fin]
   int64_t plane;    // N*M*Fin
   float* yp;        // [G][N*M][Fout] partial y per group, or NULL (basis only)
+  unsigned long long* ts;  // ablation build: phase stamps (CG_TS), else NULL
 };
 
 template <int NOT>  // 32-wide output tiles (Fout <= 32 * NOT)
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
   int n, g;
   grp_map(blockIdx.x, A.G, n, g);
   if (n >= A.N) return;  // grid padded to whole XCD rounds (uniform per workgroup)
+  CG_TS(A.ts, 0);
   const int M = A.M, K = A.K, Fin = A.Fin, Fout = A.Fout;
   float* slot = smem;                     // [Mr][16]
   float* s_W = slot + A.Mr * kGQ16;       // [K][s 8][hh 2][NOT][i 32]
@@ -327,6 +329,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
       __syncthreads();
     }
   }
+  CG_TS(A.ts, 2);
   if (!want_y) return;
   // lane (row, hh) holds outputs ot*32 + 8q + 4hh + m (q = e / 4, m = e % 4)
   float* yg = A.yp + int64_t(g) * A.N * M * Fout;
@@ -350,6 +353,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
         }
       }
   }
+  CG_TS(A.ts, 3);
 }
 
 // y = act(sum_g yp[g] + res), groups added in order (bitwise reproducible)
@@ -516,6 +520,7 @@ struct GrpClenDyArgs {
   float* dx;        // [N][M][Fin]
   int dx_acc;
   int pipe;  // 1: the next group's tiles during this group's steps; 0: each group's up front
+  unsigned long long* ts;  // ablation build: phase stamps (CG_TS), else NULL
 };
 
 template <int KC2>  // Fout / 2: the row GEMM's inner half (16 or 32)
@@ -528,6 +533,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
   int n, g;
   grp_map(blockIdx.x, A.G, n, g);
   if (n >= A.N) return;
+  CG_TS(A.ts, 0);
   const int M = A.M, K = A.K, Fin = A.Fin;
   constexpr int Fout = 2 * KC2;
   constexpr int WS = Fout + 4;  // LDS row stride of the staged W rows
@@ -561,6 +567,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
   }
   if (tid < 2 * kGQ) (tid < kGQ ? slotA : slotB)[M * kGQ + (tid & (kGQ - 1))] = 0.f;  // zero row M
   __syncthreads();
+  CG_TS(A.ts, 1);
   const int bsrc = ((lane >> 1) + 32 * (lane & 1)) * 4;  // ds_bpermute source of lane 2n + h
   const bool mfma_first = wave < 4;
   // dy operand of tile rt (the MFMA lane's half row: KC2 floats), loaded ahead
@@ -691,14 +698,20 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
     }
     if (more) handover(acc, 0, !odd);
   };
+  int gi = 0;  // order groups done (phase stamps 2.. of the ablation build)
   for (int kg = ktop;;) {
     run_group(kg, IntC<0>{});
+    if (gi < 5) CG_TS(A.ts, 2 + gi);
+    ++gi;
     if (kg < 4) break;
     kg -= 4;
     run_group(kg, IntC<1>{});
+    if (gi < 5) CG_TS(A.ts, 2 + gi);
+    ++gi;
     if (kg < 4) break;
     kg -= 4;
   }
+  (void)gi;
 #pragma unroll
   for (int rt = 0; rt < kGRT; ++rt) {
     if (!rv[rt]) continue;
@@ -710,6 +723,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
     }
     *d = o;
   }
+  CG_TS(A.ts, 7);
 }
 
 }  // namespace
@@ -764,7 +778,10 @@ hipError_t launch_grp_fwd(const int* rowptr, const int* col, const float* val, c
                    grp16_fwd_lds(M, K, Fout, nnz) <= size_t(kLdsBytes);
   const int G = Fin / (g16 ? kGQ16 : kGQ);
   GrpFwdArgs a{rowptr, col, val, order, M, rup(M + 1, 32), Fin, K, Fout, N, int(nnz), G, x, W, basis,
-               int64_t(N) * M * Fin, y ? yp : nullptr};
+               int64_t(N) * M * Fin, y ? yp : nullptr, nullptr};
+#ifdef CG_DEBUG
+  a.ts = g_debug_ts;
+#endif
   const size_t lds = g16 ? grp16_fwd_lds(M, K, Fout, nnz) : grp_fwd_lds(M, K, Fout, nnz);
   if (g16 && Fout <= 32) {
     static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp16_fwd<1>),
@@ -836,7 +853,10 @@ hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* 
     return (e && e[0] == '2') ? 0 : 1;
   }();
   GrpClenDyArgs a{trowptr, tcol, tval, order, M, rup(M + 1, 32), Fin, K, N, int(nnzT), G, Fout,
-                  Fout / 2, dy, W, dx, dx_acc, pipe};
+                  Fout / 2, dy, W, dx, dx_acc, pipe, nullptr};
+#ifdef CG_DEBUG
+  a.ts = g_debug_ts;
+#endif
   static hipError_t at16 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen_dy<16>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   static hipError_t at32 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen_dy<32>),
