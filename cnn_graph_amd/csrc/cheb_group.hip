@@ -382,6 +382,9 @@ struct GrpClenArgs {
   int dx_acc;
 };
 
+// PC: the rows' columns packed in registers (lds_row_spmm_pc) for rows of at
+// most 12 entries, the CSR columns read from LDS per step otherwise
+template <bool PC>
 __global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -428,6 +431,13 @@ __global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
     off[rt] = (int64_t(n) * M + (rv[rt] ? row[rt] : 0)) * Fin + c0;
     wl[rt] = wave_max(re[rt] - rb[rt]);
   }
+  constexpr int NP = PC ? 6 : 1;
+  unsigned pk[kGRT][NP];
+  if (PC) {
+    __syncthreads();  // s_col staged
+#pragma unroll
+    for (int rt = 0; rt < kGRT; ++rt) pack_row_cols<NP>(pk[rt], s_col, rb[rt], re[rt], M);
+  }
   loadD(K - 1);
   // G_{K-1} = D_{K-1} + c * (+0)  (k_clenshaw_step's expression with no G_K)
   const float cl = (K - 1 >= 1) ? 2.f : 1.f;
@@ -460,10 +470,21 @@ __global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
 #pragma unroll
     for (int rt = 0; rt < kGRT; ++rt) {
       float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (rv[rt])
-        with_row_len(wl[rt], [&](auto lc) {
-          sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
-        });
+      if (rv[rt]) {
+        if constexpr (PC) {
+          with_row_len(wl[rt], [&](auto lc) {
+            constexpr int LL = decltype(lc)::value;
+            if constexpr (LL > 0 && LL <= 2 * NP)
+              sm = lds_row_spmm_pc<LL, NP, 3>(cur, 4 * hh, pk[rt], s_val, rb[rt], re[rt]);
+            else
+              sm = lds_row_spmm<LL>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+          });
+        } else {
+          with_row_len(wl[rt], [&](auto lc) {
+            sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+          });
+        }
+      }
       const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
@@ -817,10 +838,18 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
   const int G = Fin / kGQ;
   GrpClenArgs a{trowptr, tcol, tval, order, M, rup(M + 1, 32), Fin, K, N, int(nnzT), G, D,
                 int64_t(N) * M * Fin, dx, dx_acc};
-  static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-  if (at != hipSuccess) return at;
-  hipLaunchKernelGGL(k_grp_clen, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
+  static hipError_t at0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen<false>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+  static hipError_t at1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen<true>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+  if (at0 != hipSuccess) return at0;
+  if (at1 != hipSuccess) return at1;
+  // CG_GRP_PC=0: columns read from LDS every step (A/B; dx bitwise the same)
+  const char* pc = getenv("CG_GRP_PC");
+  if (pc && pc[0] == '0')
+    hipLaunchKernelGGL(k_grp_clen<false>, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
+  else
+    hipLaunchKernelGGL(k_grp_clen<true>, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
   return hipGetLastError();
 }
 

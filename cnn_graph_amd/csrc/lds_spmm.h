@@ -55,6 +55,50 @@ __device__ __forceinline__ float4 lds_row_spmm(const float* X, int stride, int c
   return s;
 }
 
+// The same product with the row's columns already in registers: pk holds the
+// row's (up to 2*NP) column indices packed two per word (entry e in bits
+// 16*(e & 1) of pk[e / 2]; entries past the row hold zrow).  The gathers no
+// longer wait on an LDS read of the column, and the row takes L LDS gathers +
+// L value reads instead of 3L reads; sum order and padding (+0 for w = 0)
+// exactly lds_row_spmm's.  SH = log2(stride).
+template <int L, int NP, int SH>
+__device__ __forceinline__ float4 lds_row_spmm_pc(const float* X, int c0, const unsigned (&pk)[NP],
+                                                  const float* val, int rb, int re) {
+#pragma clang fp contract(off)
+  static_assert(L <= 2 * NP, "row longer than the packed columns");
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  float w[L];
+  float4 g[L];
+#pragma unroll
+  for (int e = 0; e < L; ++e) {
+    const bool ok = rb + e < re;
+    w[e] = ok ? val[rb + e] : 0.f;
+    const int c = int((pk[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+    g[e] = *reinterpret_cast<const float4*>(X + (c << SH) + c0);
+  }
+#pragma unroll
+  for (int e = 0; e < L; ++e) {
+    s.x = s.x + w[e] * g[e].x;
+    s.y = s.y + w[e] * g[e].y;
+    s.z = s.z + w[e] * g[e].z;
+    s.w = s.w + w[e] * g[e].w;
+  }
+  return s;
+}
+
+// pk for lds_row_spmm_pc: the columns of CSR row entries [rb, re), padded with zrow
+template <int NP>
+__device__ __forceinline__ void pack_row_cols(unsigned (&pk)[NP], const unsigned short* col, int rb,
+                                              int re, int zrow) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int e0 = rb + 2 * p, e1 = e0 + 1;
+    const unsigned lo = e0 < re ? unsigned(col[e0]) : unsigned(zrow);
+    const unsigned hi = e1 < re ? unsigned(col[e1]) : unsigned(zrow);
+    pk[p] = lo | (hi << 16);
+  }
+}
+
 template <int V>
 struct IntC {
   static constexpr int value = V;

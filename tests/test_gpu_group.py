@@ -98,3 +98,31 @@ def test_group_clenshaw_fused_dx_accumulate(dev):
     torch.cuda.synchronize()
     assert torch.equal(dxa, ref)
     assert torch.equal(dW, r.dW)
+
+
+@pytest.mark.parametrize("gname,N,Fin,K,Fout", [("golden_E.npz", 3, 32, 20, 24), ("golden_B.npz", 2, 16, 5, 40)])
+def test_group_clenshaw_packed_columns_bitwise(dev, monkeypatch, gname, N, Fin, K, Fout):
+    """k_grp_clen (the dBasis-planes variant, Fout outside the fused kernel's
+    2 / 32 / 64) with the rows' columns packed in registers (default) and read
+    from LDS every step (CG_GRP_PC=0): dx bitwise equal to each other and to
+    the steps path."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden(gname))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    rng = np.random.default_rng(N + Fin + K + Fout)
+    xt = _t(rng.standard_normal((N, M, Fin)), dev)
+    Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
+    dyt = _t(rng.standard_normal((N, M, Fout)), dev)
+    out = {}
+    for name, variant, pc in (("pc", "auto", "1"), ("lds", "auto", "0"), ("steps", "steps", "1")):
+        monkeypatch.setenv("CG_GRP_PC", pc)
+        plan = ChebPlan(Lt, device=0, path="stream", variant=variant)
+        r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
+        r.forward(xt, Wt)
+        r.backward(dyt, Wt)
+        torch.cuda.synchronize()
+        out[name] = r.dx.clone()
+    assert torch.equal(out["pc"], out["lds"])
+    assert torch.equal(out["pc"], out["steps"])
