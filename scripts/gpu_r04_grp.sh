@@ -21,6 +21,8 @@ for rep in 1 2; do
   done
 done
 for v in 2 1; do echo "== CG_SEQ_V=$v"; cut -c1-200 $O/E_seq$v.jsonl; done
+for v in 2 1; do CG_SEQ_V=$v timeout -k 10 200 python3 scripts/stamps_E.py >> $O/stampsE.jsonl 2>> $O/E.err || { tail -5 $O/E.err; exit 1; }; done
+cat $O/stampsE.jsonl
 bash scripts/gpu_r04_lds.sh ${1:-r04_grp}/lds > $O/lds.log 2>&1 || { tail -20 $O/lds.log; exit 1; }
 tail -40 $O/lds.log
 echo DONE
