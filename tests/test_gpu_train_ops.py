@@ -41,9 +41,13 @@ def test_dropout_formula_mask_and_rate(dev):
     kept = int(mask.sum())
     # binomial(n, 0.8): 6 sigma
     assert abs(kept - keep * n) < 6 * math.sqrt(n * keep * (1 - keep))
-    k32 = torch.tensor(keep, dtype=torch.float32)
-    assert torch.equal(y[mask], x[mask] / k32)
-    assert torch.equal(xa.grad, (dy * mask.float()) / k32)
+    # IEEE fp32 division on the host (torch divides a GPU tensor by a CPU scalar
+    # as a multiply by its reciprocal, which is not the formula)
+    k32 = np.float32(keep)
+    xn, yn, mn = x.cpu().numpy(), y.detach().cpu().numpy(), mask.cpu().numpy()
+    assert np.array_equal(yn[mn], xn[mn] / k32) and not yn[~mn].any()
+    dyn = dy.cpu().numpy()
+    assert np.array_equal(xa.grad.cpu().numpy(), (dyn * mn.astype(np.float32)) / k32)
     # deterministic in the seed, another seed another mask
     assert torch.equal(ops.dropout(x, keep, 1234), y.detach())
     assert not torch.equal(ops.dropout(x, keep, 1235) != 0, mask)
