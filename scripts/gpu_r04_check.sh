@@ -9,9 +9,10 @@ O=gpurun_out/${1:-r04_check}
 mkdir -p $O
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')" > $O/smoke.txt 2>&1 || { cat $O/smoke.txt; exit 1; }
 tail -1 $O/smoke.txt
-timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v -rP --tb=short --timeout 240 --timeout-method thread > $O/pytest.txt 2>&1; rc=$?
+timeout -k 10 1100 python -u -m pytest tests -m gpu -v -rP --tb=short --timeout 240 --timeout-method thread > $O/pytest.txt 2>&1; rc=$?
 grep -E "passed|failed" $O/pytest.txt | tail -2
-[ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $O/pytest.txt | head -30; exit 1; }
+# a failing assertion is reported and the pass goes on; a hang / crash (timeout, signal) ends it
+[ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $O/pytest.txt | head -30; [ $rc -eq 1 ] || exit 1; }
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
 cut -c1-400 $O/bench.json
 echo DONE
