@@ -47,6 +47,27 @@ constexpr int debug_flags() { return 0; }
 #define CG_TS(ts, slot) ((void)0)
 #endif
 
+// Stage n values into LDS with U loads in flight per thread: the plain
+// `for (e = tid; e < n; e += NT) lds[e] = ld(e)` loop is compiled load ->
+// s_waitcnt vmcnt(0) -> ds_write per iteration (one L2 round trip each; 20 of
+// them for a K = 20 weight block).  Same values, same places.
+template <int U, int NT, typename LD, typename ST>
+__device__ __forceinline__ void stage_lds(int n, LD&& ld, ST&& st) {
+  for (int e0 = int(threadIdx.x); e0 < n; e0 += U * NT) {
+    float v[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e = e0 + q * NT;
+      v[q] = e < n ? ld(e) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e = e0 + q * NT;
+      if (e < n) st(e, v[q]);
+    }
+  }
+}
+
 // ---- resident (LDS) path ---------------------------------------------------
 struct ResidentGeom {
   int nnz;         // nonzeros of L~ (== of L~^T); the resident path needs nnz >= 1

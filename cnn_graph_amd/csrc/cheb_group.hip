@@ -84,12 +84,12 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
   const bool want_y = A.yp != nullptr;
   if (want_y) {
-    for (int e = tid; e < K * 256 * NOT; e += kGT) {
+    stage_lds<8, kGT>(K * 256 * NOT, [&](int e) {
       const int i = e & 31, ot = (e >> 5) % NOT, h2 = (e / (32 * NOT)) & 1;
       const int s = (e / (64 * NOT)) & 3, k = e / (256 * NOT);
       const int ch = kGQ * g + 4 * h2 + s, out = ot * 32 + i;
-      s_W[e] = out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
-    }
+      return out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
+    }, [&](int e, float v) { s_W[e] = v; });
   }
   for (int e = tid; e < A.nnz; e += kGT) {
     s_val[e] = A.val[e];
@@ -225,12 +225,12 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
   const bool want_y = A.yp != nullptr;
   if (want_y) {
-    for (int e = tid; e < K * 512 * NOT; e += kGT) {
+    stage_lds<8, kGT>(K * 512 * NOT, [&](int e) {
       const int i = e & 31, ot = (e >> 5) % NOT, h2 = (e / (32 * NOT)) & 1;
       const int s = (e / (64 * NOT)) & 7, k = e / (512 * NOT);
       const int ch = kGQ16 * g + 8 * h2 + s, out = ot * 32 + i;
-      s_W[e] = out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
-    }
+      return out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
+    }, [&](int e, float v) { s_W[e] = v; });
   }
   for (int e = tid; e < A.nnz; e += kGT) {
     s_val[e] = A.val[e];
@@ -568,10 +568,10 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
     s_val[e] = A.tval[e];
     s_col[e] = static_cast<unsigned short>(A.tcol[e]);
   }
-  for (int e = tid; e < K * kGQ * Fout; e += kGT) {
+  stage_lds<8, kGT>(K * kGQ * Fout, [&](int e) {
     const int f = e % Fout, kc = e / Fout, ch = kc % kGQ, k = kc / kGQ;
-    s_w[kc * WS + f] = A.W[(int64_t(c0 + ch) * K + k) * Fout + f];
-  }
+    return A.W[(int64_t(c0 + ch) * K + k) * Fout + f];
+  }, [&](int e, float v) { s_w[(e / Fout) * WS + e % Fout] = v; });
   int row[kGRT], rb[kGRT], re[kGRT], wl[kGRT];
   bool rv[kGRT];
   int drow[kGRT];  // the MFMA lane's tile row (graph row of column mi), -1 past M

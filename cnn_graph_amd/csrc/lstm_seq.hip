@@ -216,22 +216,22 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
   // A operands of the transposed contraction: lane (i, hh) of MFMA step s in
   // quarter q, order k holds Wh[(8q + 4hh + s) K + k][gate column of tile
   // row i] -- tile ct's rows i = 8 g + m are gate g, unit 16u + 8ct + m
-  for (int e = tid; e < K * 2048; e += kST) {
+  stage_lds<8, kST>(K * 2048, [&](int e) {
     const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3;
     const int q = (e >> 9) & 3, k = e >> 11;
     const int ch = 8 * q + 4 * h2 + s;
     const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
-    s_W[e] = A.Wh[int64_t(ch * K + k) * 128 + gcol];
-  }
+    return A.Wh[int64_t(ch * K + k) * 128 + gcol];
+  }, [&](int e, float v) { s_W[e] = v; });
   if (A.xs) {
     // x channel c = 2s + hh of MFMA step s (zero past Fin): Fin <= 2 needs
     // one step per order, not four
-    for (int e = tid; e < K * 512; e += kST) {
+    stage_lds<8, kST>(K * 512, [&](int e) {
       const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3, k = e >> 9;
       const int c = 2 * s + h2;
       const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
-      s_Wx[e] = c < A.Fin ? A.Wx[int64_t(c * K + k) * 128 + gcol] : 0.f;
-    }
+      return c < A.Fin ? A.Wx[int64_t(c * K + k) * 128 + gcol] : 0.f;
+    }, [&](int e, float v) { s_Wx[e] = v; });
   }
   for (int e = tid; e < 128; e += kST) s_b[e] = A.bias ? A.bias[e] : 0.f;
   for (int e = tid; e < A.nnz; e += kST) {
@@ -615,20 +615,20 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
   float* s_b = s_Wx + (A.xs ? K * 512 : 0);
   float* s_val = s_b + 128;
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
-  for (int e = tid; e < K * 2048; e += kST) {
+  stage_lds<8, kST>(K * 2048, [&](int e) {
     const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3;
     const int q = (e >> 9) & 3, k = e >> 11;
     const int ch = 8 * q + 4 * h2 + s;
     const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
-    s_W[e] = A.Wh[int64_t(ch * K + k) * 128 + gcol];
-  }
+    return A.Wh[int64_t(ch * K + k) * 128 + gcol];
+  }, [&](int e, float v) { s_W[e] = v; });
   if (A.xs) {
-    for (int e = tid; e < K * 512; e += kST) {
+    stage_lds<8, kST>(K * 512, [&](int e) {
       const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3, k = e >> 9;
       const int c = 2 * s + h2;
       const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
-      s_Wx[e] = c < A.Fin ? A.Wx[int64_t(c * K + k) * 128 + gcol] : 0.f;
-    }
+      return c < A.Fin ? A.Wx[int64_t(c * K + k) * 128 + gcol] : 0.f;
+    }, [&](int e, float v) { s_Wx[e] = v; });
   }
   for (int e = tid; e < 128; e += kST) s_b[e] = A.bias ? A.bias[e] : 0.f;
   for (int e = tid; e < A.nnz; e += kST) {
@@ -932,10 +932,10 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
   // A operand of MFMA step s, order o: lane (i, q) holds Wh[(16u + i) K + o][g]
   // with g the gate column (s % 4) * 32 + 8q + s / 4 -- the column whose dpre
   // lane (row, q) supplies as the B operand at that step
-  for (int e = tid; e < K * 2048; e += kST) {
+  stage_lds<8, kST>(K * 2048, [&](int e) {
     const int i = e & 15, qq = (e >> 4) & 3, s = (e >> 6) & 31, o = e >> 11;
-    s_W[e] = A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
-  }
+    return A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
+  }, [&](int e, float v) { s_W[e] = v; });
   for (int e = tid; e < A.nnz; e += kST) {
     s_val[e] = A.tval[e];
     s_col[e] = static_cast<unsigned short>(A.tcol[e]);
