@@ -793,17 +793,21 @@ __global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
   const int64_t npairs = (c1 - c0 + 1) >> 1;
   TA ra[PD][NLA];
   TB rb[PD][NLB];
-  auto fetch = [&](int s, int64_t p) {  // row pair p into ring slot s (zeros past the chunk)
+  bool rvs[PD];
+  // row pair p into ring slot s, RAW: the loads are unconditional (a row past
+  // the chunk reads the chunk's first row, an idle column column 0) and the
+  // zeros are selected in consume(), one loop iteration later.  A select next
+  // to its load lets the compiler sink the load into a branch on the row's
+  // validity with a vmcnt(0) wait behind it -- which serialises the ring.
+  auto fetch = [&](int s, int64_t p) {
     const bool rv = c0 + 2 * p + h < c1;
-    const int64_t ob = 2 * p * int64_t(A.ldd);
+    rvs[s] = rv;
+    const int64_t ro = rv ? 2 * p : -int64_t(h);  // row c0 + h + ro (row c0 when idle)
 #pragma unroll
-    for (int q = 0; q < NLA; ++q) {
-      ra[s][q] = (rv && av[q]) ? *reinterpret_cast<const TA*>(pa[q] + 2 * p * lst[q]) : TA{};
-      if constexpr (VA == 1)
-        if (aone[q]) ra[s][q] = rv ? 1.f : 0.f;
-    }
+    for (int q = 0; q < NLA; ++q) ra[s][q] = *reinterpret_cast<const TA*>(pa[q] + ro * lst[q]);
 #pragma unroll
-    for (int q = 0; q < NLB; ++q) rb[s][q] = (rv && bv[q]) ? *reinterpret_cast<const TB*>(pb[q] + ob) : TB{};
+    for (int q = 0; q < NLB; ++q)
+      rb[s][q] = *reinterpret_cast<const TB*>(pb[q] + ro * int64_t(A.ldd));
   };
   f32x16 acc[NA][NB];
 #pragma unroll
@@ -814,22 +818,43 @@ __global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 #pragma unroll
   for (int s = 0; s < PD; ++s) fetch(s, s);
-  for (int64_t p0 = 0; p0 < npairs; p0 += PD) {
+  // full rounds of PD pairs with no control flow (the compiler then counts the
+  // ring's loads: each MFMA group waits only for its own slot), then the tail;
+  // a pair past the chunk (p >= npairs) is never consumed; the missing row of
+  // an odd chunk's last pair and idle columns enter as zeros
+  auto consume = [&](int s) {
+    const bool rv = rvs[s];
+    float y[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float v = dw_el<VB>(rb[s][b / VB], b % VB);
+      y[b] = (rv && bv[b / VB]) ? v : 0.f;
+    }
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      float x = dw_el<VA>(ra[s][a / VA], a % VA);
+      x = (rv && av[a / VA]) ? x : 0.f;
+      if constexpr (VA == 1) x = aone[a] ? (rv ? 1.f : 0.f) : x;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y[b], acc[a][b], 0, 0, 0);
+    }
+  };
+  const int64_t nfull = npairs / PD * PD;
+  for (int64_t p0 = 0; p0 < nfull; p0 += PD) {
 #pragma unroll
     for (int s = 0; s < PD; ++s) {
-      if (p0 + s < npairs) {
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-          const float x = dw_el<VA>(ra[s][a / VA], a % VA);
-#pragma unroll
-          for (int b = 0; b < NB; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(x, dw_el<VB>(rb[s][b / VB], b % VB),
-                                                             acc[a][b], 0, 0, 0);
-        }
-        if (p0 + s + PD < npairs) fetch(s, p0 + s + PD);
-      }
+      consume(s);
+      fetch(s, p0 + s + PD);
+      // keep slot s's loads right behind its MFMAs (a rolling ring); the
+      // scheduler otherwise hoists every MFMA of the round ahead of all the
+      // round's loads, and the next round waits out a whole memory latency
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
+#pragma unroll
+  for (int s = 0; s < PD; ++s)
+    if (nfull + s < npairs) consume(s);
   // tile (a, b), accumulator r: A lane i = (r & 3) + 8 (r >> 2) + 4 h, B lane li
   const int FinK = A.FinK;
 #pragma unroll
@@ -1086,7 +1111,7 @@ static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int
     if (mfmas(2) < mfmas(3)) return go(k_dw_direct<1, 2, 2, 2, 10>, 2);
     return go(k_dw_direct<1, 3, 2, 2, 8>, 3);
   }
-  return go(k_dw_direct<1, 2, 2, 4, 6>, 2);
+  return go(k_dw_direct<1, 1, 2, 4, 8>, 1);
 }
 
 static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int64_t R, int FinKh,

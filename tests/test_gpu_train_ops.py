@@ -105,7 +105,10 @@ def test_clip_by_norm_and_check_numerics(dev):
         r64 = ref.astype(np.float64)
         nrm = np.sqrt((r64 * r64).sum())
         assert O.normwise_err(t.cpu().numpy(), r64 * 5.0 / max(nrm, 5.0)) < 1e-6
-    assert torch.equal(tb, torch.from_numpy(b).to(dev) * 5.0 / 5.0)  # norm < 5: unchanged
+    # norm < 5: t = (t*5)/max(norm, 5) = (t*5)/5 in IEEE fp32 (numpy divides
+    # correctly rounded; torch's tensor / scalar multiplies by the reciprocal)
+    f5 = np.float32(5.0)
+    assert np.array_equal(tb.cpu().numpy(), (b * f5) / f5)
     bad = torch.ones((100,), device=dev)
     bad[17] = float("nan")
     with pytest.raises(FloatingPointError):
