@@ -205,14 +205,16 @@ int build_slots(cg_plan::Slots* out, int32_t M, const int32_t* rp, const int32_t
 // FastImage): thread->row assignment and bank-aware record layout from
 // lds_layout.cpp, uploaded as one device allocation.
 int build_fast_image(cg_plan::Fast* out, int32_t M, const int32_t* rp, const int32_t* ci,
-                     const float* v) {
+                     const float* v, cg::FastLayout* keep = nullptr, const cg::FastLayout* reuse = nullptr) {
   constexpr int kT = 1024, kWd = cg::kFastWidth;
   if (M > kT) return CG_OK;
   int maxlen = 0;
   for (int32_t r = 0; r < M; ++r) maxlen = std::max(maxlen, rp[r + 1] - rp[r]);
   if (maxlen > kWd) return CG_OK;
   cg::FastLayout lay;
-  cg::plan_fast_layout(M, rp, ci, &lay);
+  if (reuse) lay = *reuse;  // the same sparsity pattern: the same layout
+  else cg::plan_fast_layout(M, rp, ci, &lay);
+  if (keep) *keep = lay;
   std::vector<float> val(size_t(kWd) * kT, 0.f);
   for (int t = 0; t < kT; ++t) {
     const int r = lay.row[size_t(t)];
@@ -587,8 +589,15 @@ int cg_plan_create(cg_plan** plan, int device, int32_t M, int64_t nnz, const int
   }
   if (!rc && nnz > 0) rc = build_slots(&p->slots, M, rowptr, col, val);
   if (!rc && nnz > 0) rc = build_slots(&p->tslots, M, trp.data(), tci.data(), tv.data());
-  if (!rc && nnz > 0) rc = build_fast_image(&p->fast, M, rowptr, col, val);
-  if (!rc && nnz > 0) rc = build_fast_image(&p->tfast, M, trp.data(), tci.data(), tv.data());
+  // a symmetric pattern (every Laplacian here) shares one layout between L~
+  // and L~^T: the annealing (lds_layout.cpp) runs once
+  const bool sym = nnz > 0 && std::equal(rowptr, rowptr + M + 1, trp.begin()) &&
+                   std::equal(col, col + nnz, tci.begin());
+  cg::FastLayout lay;
+  if (!rc && nnz > 0) rc = build_fast_image(&p->fast, M, rowptr, col, val, sym ? &lay : nullptr);
+  if (!rc && nnz > 0)
+    rc = build_fast_image(&p->tfast, M, trp.data(), tci.data(), tv.data(), nullptr,
+                          sym && p->fast.ok ? &lay : nullptr);
   (void)hipSetDevice(prev);
   if (rc) {
     free_plan(p);

@@ -1077,7 +1077,8 @@ int dw_chunks(int64_t R) {
 // columns of the slice decide the B loads (VB, NLB), the basis columns (with
 // the LSTM's x-plane and ones columns) are cut into G groups of NA = VA*NLA
 // virtual tiles, NA chosen for the fewest MFMAs per row pair (G*NA*NB);
-// CG_DW_DIRECT=0 keeps k_dw_slabs (A/B runs), =2 prefers two-float basis loads
+// CG_DW_DIRECT=0 keeps k_dw_slabs (A/B runs), =2 prefers two-float basis loads,
+// =3 forces k_dw_direct whatever the wave count (tests; so does 2)
 static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
                              int ldd, float* slab, hipStream_t s, int pl_fin, int64_t pl_stride,
                              int K, int chunks, int64_t rpc, const float* xb, int x_fin,
@@ -1096,6 +1097,10 @@ static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int
   auto go = [&](auto kern, int na) {
     a.G = (FinK + 32 * na - 1) / (32 * na);
     const int64_t waves = int64_t(chunks) * a.G;
+    // one wave per SIMD at least (its ~300-500 VGPRs allow no second one):
+    // below that k_dw_slabs' LDS-batched waves win (config R: 800 waves,
+    // 4.87 vs 5.10 ms per step, profiles/r04_ab)
+    if (mode == 1 && waves < 1024) return false;
     hipLaunchKernelGGL(kern, dim3(unsigned((waves + 3) / 4)), dim3(256), 0, s, a);
     *err = hipGetLastError();
     return true;

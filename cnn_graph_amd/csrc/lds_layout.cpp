@@ -49,51 +49,103 @@ struct Group {
   float weight;
 };
 
-// Greedy copy assignment for one group; returns the max bank load.
-int group_cost(const Group& g, const std::vector<int8_t>& b0, const std::vector<int8_t>& b1,
-               int* choice /* may be null */) {
-  int load[kBanks] = {0};
-  const int n = int(g.verts.size());
-  int chs[64];
-  if (g.copy >= 0) {
-    const std::vector<int8_t>& b = g.copy ? b1 : b0;
-    for (int i = 0; i < n; ++i) load[b[size_t(g.verts[size_t(i)])]]++;
-  } else {
-    for (int i = 0; i < n; ++i) {
-      const int v = g.verts[size_t(i)];
-      const int x = b0[size_t(v)], y = b1[size_t(v)];
-      const int c = load[x] <= load[y] ? 0 : 1;
-      chs[i] = c;
-      load[c ? y : x]++;
-    }
-    for (int pass = 0; pass < 2; ++pass) {
-      bool moved = false;
-      for (int i = 0; i < n; ++i) {
-        const int v = g.verts[size_t(i)];
-        const int cur = chs[i] ? b1[size_t(v)] : b0[size_t(v)];
-        const int alt = chs[i] ? b0[size_t(v)] : b1[size_t(v)];
-        if (load[alt] + 1 < load[cur]) {
-          load[cur]--;
-          load[alt]++;
-          chs[i] ^= 1;
-          moved = true;
+// augmenting paths of the b-matching in group_cost: vertex x into one of its
+// two candidate banks of capacity cap, displacing (recursively) a vertex that
+// can move to its other bank
+struct Aug {
+  const int (*cand)[2];
+  int cap;
+  int fill[kBanks] = {0};
+  int slot[kBanks][64];
+  bool vis[kBanks];
+  bool run(int x, int* c2) {
+    for (int e = 0; e < 2; ++e) {
+      const int bk = cand[x][e];
+      if (vis[bk]) continue;
+      vis[bk] = true;
+      if (fill[bk] < cap) {
+        slot[bk][fill[bk]++] = x;
+        c2[x] = e;
+        return true;
+      }
+      for (int q = 0; q < fill[bk]; ++q) {
+        const int y = slot[bk][q];
+        if (run(y, c2)) {  // y moved to its other bank
+          slot[bk][q] = x;
+          c2[x] = e;
+          return true;
         }
       }
-      if (!moved) break;
     }
-    if (choice)
-      for (int i = 0; i < n; ++i) choice[i] = chs[i];
+    return false;
   }
-  // free lanes take the emptiest banks
-  for (int f = 0; f < g.nfree; ++f) {
-    int best = 0;
-    for (int b = 1; b < kBanks; ++b)
-      if (load[b] < load[best]) best = b;
-    load[best]++;
+};
+
+// Copy assignment for one group with the smallest max bank load (free lanes
+// included): a greedy start, then, while the max load exceeds the lower bound,
+// an exact check by augmenting paths whether every vertex fits in banks of
+// capacity cap = bound, bound + 1, ... (each vertex has two candidate banks,
+// so this is a bipartite b-matching).  Returns the max bank load.
+int group_cost(const Group& g, const std::vector<int8_t>& b0, const std::vector<int8_t>& b1,
+               int* choice /* may be null */) {
+  const int n = int(g.verts.size());
+  int cand[64][2];
+  int nd = 0;  // distinct candidates
+  for (int i = 0; i < n; ++i) {
+    const int v = g.verts[size_t(i)];
+    cand[i][0] = b0[size_t(v)];
+    cand[i][1] = g.copy >= 0 ? (g.copy ? b1[size_t(v)] : b0[size_t(v)]) : b1[size_t(v)];
+    if (g.copy == 1) cand[i][0] = cand[i][1];
+    nd += cand[i][0] != cand[i][1];
   }
-  int mx = 0;
-  for (int b = 0; b < kBanks; ++b) mx = std::max(mx, load[b]);
-  return mx;
+  int chs[64];
+  int load[kBanks] = {0};
+  for (int i = 0; i < n; ++i) {  // greedy
+    const int c = load[cand[i][0]] <= load[cand[i][1]] ? 0 : 1;
+    chs[i] = c;
+    load[cand[i][c]]++;
+  }
+  auto finish = [&](int* ld) {
+    for (int f = 0; f < g.nfree; ++f) {  // free lanes take the emptiest banks
+      int best = 0;
+      for (int b = 1; b < kBanks; ++b)
+        if (ld[b] < ld[best]) best = b;
+      ld[best]++;
+    }
+    int mx = 0;
+    for (int b = 0; b < kBanks; ++b) mx = std::max(mx, ld[b]);
+    return mx;
+  };
+  int tmp[kBanks];
+  std::copy(load, load + kBanks, tmp);
+  int best = finish(tmp);
+  const int bound = (n + g.nfree + kBanks - 1) / kBanks;
+  if (best > bound && nd > 0) {
+    for (int cap = bound; cap < best; ++cap) {
+      // b-matching of vertices to banks of capacity cap (free lanes fit when
+      // some bank stays below cap, i.e. n + nfree <= 32 cap)
+      if (n + g.nfree > kBanks * cap) continue;
+      int c2[64];
+      Aug m{cand, cap};
+      bool ok = true;
+      for (int i = 0; i < n && ok; ++i) {
+        std::fill(m.vis, m.vis + kBanks, false);
+        ok = m.run(i, c2);
+      }
+      if (!ok) continue;
+      int ld[kBanks] = {0};
+      for (int i = 0; i < n; ++i) ld[cand[i][c2[i]]]++;
+      const int mx = finish(ld);
+      if (mx < best) {
+        best = mx;
+        std::copy(c2, c2 + n, chs);
+      }
+      break;
+    }
+  }
+  if (choice)
+    for (int i = 0; i < n; ++i) choice[i] = g.copy >= 0 ? g.copy : chs[i];
+  return best;
 }
 
 }  // namespace
@@ -175,10 +227,29 @@ void plan_fast_layout(int M, const int32_t* rp, const int32_t* ci, FastLayout* o
     for (int v : groups[size_t(gi)].verts) vgroups[size_t(v)].push_back(gi);
 
   // ---- annealing over bank classes ----------------------------------------------
+  // The two own-record writes of a 32-lane half are conflict-free by
+  // construction: within every half the rows' copy-0 classes are a set of
+  // distinct banks, and so are their copy-1 classes, and the annealing moves
+  // keep it so (swap two rows' classes of one copy inside a half, or move a
+  // row to a class its half leaves unused).  The gathers and the MFMA tile
+  // reads are what it optimises.
   std::vector<int8_t> b0(static_cast<size_t>(M)), b1(static_cast<size_t>(M));
-  for (int v = 0; v < M; ++v) {
-    b0[size_t(v)] = int8_t(v % kBanks);
-    b1[size_t(v)] = int8_t((v * 7 + 13) % kBanks);
+  std::vector<int> half_of(static_cast<size_t>(M), -1);
+  std::vector<std::vector<int>> half_rows(kT / 32);
+  for (int t = 0; t < kT; ++t)
+    if (trow[size_t(t)] >= 0) {
+      half_of[size_t(trow[size_t(t)])] = t / 32;
+      half_rows[size_t(t / 32)].push_back(trow[size_t(t)]);
+    }
+  std::mt19937 rng(20170u);
+  for (auto& hr : half_rows) {
+    int perm[kBanks];
+    for (int b = 0; b < kBanks; ++b) perm[b] = b;
+    std::shuffle(perm, perm + kBanks, rng);
+    for (size_t i = 0; i < hr.size(); ++i) {
+      b0[size_t(hr[i])] = int8_t(i);
+      b1[size_t(hr[i])] = int8_t(perm[i]);
+    }
   }
   std::vector<int> gc(groups.size());
   double total = 0;
@@ -186,20 +257,31 @@ void plan_fast_layout(int M, const int32_t* rp, const int32_t* ci, FastLayout* o
     gc[gi] = group_cost(groups[gi], b0, b1, nullptr);
     total += groups[gi].weight * gc[gi];
   }
-  std::mt19937 rng(20170u);
-  const long iters = std::max<long>(200000, 120L * M);
+  const long iters = std::max<long>(400000, 400L * M);
   const double T0 = 1.0, T1 = 0.02;
-  std::vector<int> newc;
-  for (long it = 0; it < iters; ++it) {
+  // stop early at the bound: every group at its fewest possible cycles
+  double lower = 0;
+  for (const Group& g : groups)
+    lower += g.weight * ((int(g.verts.size()) + g.nfree + kBanks - 1) / kBanks);
+  std::vector<int> aff, newc;
+  for (long it = 0; it < iters && total > lower + 1e-6; ++it) {
     const double T = T0 * std::pow(T1 / T0, double(it) / double(iters));
     const int v = int(rng() % uint32_t(M));
     const int c = int(rng() & 1u);
     std::vector<int8_t>& b = c ? b1 : b0;
-    const int8_t old = b[size_t(v)];
+    const std::vector<int>& hr = half_rows[size_t(half_of[size_t(v)])];
     const int8_t nb = int8_t(rng() % kBanks);
-    if (nb == old) continue;
+    if (nb == b[size_t(v)]) continue;
+    int u = -1;  // the half's row holding class nb (swapped with v), if any
+    for (int x : hr)
+      if (b[size_t(x)] == nb) u = x;
+    const int8_t old = b[size_t(v)];
     b[size_t(v)] = nb;
-    const std::vector<int>& aff = vgroups[size_t(v)];
+    if (u >= 0) b[size_t(u)] = old;
+    aff = vgroups[size_t(v)];
+    if (u >= 0) aff.insert(aff.end(), vgroups[size_t(u)].begin(), vgroups[size_t(u)].end());
+    std::sort(aff.begin(), aff.end());
+    aff.erase(std::unique(aff.begin(), aff.end()), aff.end());
     newc.resize(aff.size());
     double d = 0;
     for (size_t q = 0; q < aff.size(); ++q) {
@@ -207,12 +289,13 @@ void plan_fast_layout(int M, const int32_t* rp, const int32_t* ci, FastLayout* o
       newc[q] = group_cost(g, b0, b1, nullptr);
       d += g.weight * (newc[q] - gc[size_t(aff[q])]);
     }
-    const double u = double(rng()) / 4294967296.0;
-    if (d <= 0 || u < std::exp(-d / T)) {
+    const double uu = double(rng()) / 4294967296.0;
+    if (d <= 0 || uu < std::exp(-d / T)) {
       for (size_t q = 0; q < aff.size(); ++q) gc[size_t(aff[q])] = newc[q];
       total += d;
     } else {
       b[size_t(v)] = old;
+      if (u >= 0) b[size_t(u)] = nb;
     }
   }
 
@@ -290,18 +373,23 @@ void plan_fast_layout(int M, const int32_t* rp, const int32_t* ci, FastLayout* o
         out->rposr[size_t(lane0 + i)] = position(r, choice[k]);
         ++k;
       }
-      // idle lanes: dummy records in distinct banks the active lanes do not use
-      std::vector<int> load(kBanks, 0);
-      for (int p : used0) load[size_t(bank_of(p))]++;
+      // idle lanes: dummy records in banks the active lanes' writes leave
+      // empty, chosen per copy (both writes stay conflict-free)
+      std::vector<int> load0(kBanks, 0), load1(kBanks, 0);
+      for (int p : used0) load0[size_t(bank_of(p))]++;
+      for (int p : used1) load1[size_t(bank_of(p))]++;
+      auto emptiest = [&](std::vector<int>& ld) {
+        int best = 0;
+        for (int b = 1; b < kBanks; ++b)
+          if (ld[size_t(b)] < ld[size_t(best)]) best = b;
+        ld[size_t(best)]++;
+        return best;
+      };
       for (int i = 0; i < 32; ++i) {
         const int t = lane0 + i;
         if (trow[size_t(t)] >= 0) continue;
-        int best = 0;
-        for (int b = 1; b < kBanks; ++b)
-          if (load[size_t(b)] < load[size_t(best)]) best = b;
-        load[size_t(best)]++;
-        out->rpos0[size_t(t)] = out->rpos1[size_t(t)] = out->rposr[size_t(t)] =
-            out->dummy_base + best;
+        out->rpos0[size_t(t)] = out->rposr[size_t(t)] = out->dummy_base + emptiest(load0);
+        out->rpos1[size_t(t)] = out->dummy_base + emptiest(load1);
       }
     }
   // MFMA tile reads

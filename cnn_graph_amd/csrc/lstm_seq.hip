@@ -120,11 +120,13 @@ __device__ __forceinline__ void bst16_sc1(__amdgpu_buffer_rsrc_t r, int off, flo
   __builtin_amdgcn_raw_buffer_store_b128(w, r, off * 4, 0, 16);
 }
 
-// CG_SEQ_V=1: the coupled kernel k_lstm_seq instead of k_lstm_seq2 (A/B runs;
-// the same outputs bitwise).  Read per launch.
+// CG_SEQ_V=2: the decoupled kernel k_lstm_seq2 instead of k_lstm_seq (A/B runs;
+// the same outputs bitwise).  k_lstm_seq is the default: config E's layer
+// forward 1.29-1.31 ms against 1.74 ms for k_lstm_seq2 (profiles/r04_ab).
+// Read per launch.
 static bool seq_v2_enabled() {
   const char* e = getenv("CG_SEQ_V");
-  return !(e && e[0] == '1');
+  return e && e[0] == '2';
 }
 
 static int seq_xpre() {

@@ -1,10 +1,14 @@
 #!/usr/bin/env python3
 """Phase stamps of config E's layer forward on the DEBUG build (CG_LIB_PATH):
-k_lstm_seq2 (default) or k_lstm_seq (CG_SEQ_V=1), step 1 of the first sample of
+k_lstm_seq (default) or k_lstm_seq2 (CG_SEQ_V=2), step 1 of the first sample of
 every pair: 0 step start, 1 own quarters' recurrence done (seq2: phase 1),
 2 partner wait done, 3 contraction + gates done (seq2: phase 2) [k_lstm_seq:
 3 all quarters contracted, 4 epilogue done].  Median over workgroups, us from
-the step start; plus the HIP-event time of the layer forward."""
+the step start; plus the HIP-event time of the layer forward.  An optional
+argument sets the debug build's ablation flags for the whole run (k_lstm_seq2
+phase 2: 1 no MFMA, 4 linear gates, 16 no gx / c loads, 64 no act stores,
+128 no c stores, 256 no h stores; outputs are garbage, times only).
+  python3 scripts/stamps_E.py [FLAGS]"""
 import ctypes
 import json
 import os
@@ -47,6 +51,9 @@ def main():
 
     h = _lib.lib()
     h.cg_debug_set_ts.argtypes = [ctypes.c_void_p]
+    flags = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    h.cg_debug_set_flags.argtypes = [ctypes.c_int]
+    h.cg_debug_set_flags(flags)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -63,7 +70,9 @@ def main():
     h.cg_debug_set_ts(None)
     ts = buf.cpu().numpy().astype(np.float64)
     d = (ts[:, 1:5] - ts[:, :1]) * 0.01
-    print(json.dumps({"kernel": "k_lstm_seq" if os.environ.get("CG_SEQ_V") == "1" else "k_lstm_seq2",
+    h.cg_debug_set_flags(0)
+    print(json.dumps({"kernel": "k_lstm_seq2" if os.environ.get("CG_SEQ_V") == "2" else "k_lstm_seq",
+                      "flags": flags,
                       "layer_fwd_ms": round(e0.elapsed_time(e1) / 5, 4),
                       "step1_us": [round(float(np.median(d[:, i])), 2) for i in range(4)]}))
 

@@ -33,7 +33,7 @@ def test_dw_direct_rows_bitwise(dev, monkeypatch, R, FK, Fo):
     D = torch.randn((R, Fo), device=dev, generator=g)
     monkeypatch.setenv("CG_DW_DIRECT", "0")
     old = ops.weight_grad(A, D)
-    monkeypatch.setenv("CG_DW_DIRECT", "1")
+    monkeypatch.setenv("CG_DW_DIRECT", "3")  # forced, whatever the wave count
     new = ops.weight_grad(A, D)
     torch.cuda.synchronize()
     assert torch.equal(new, old)
@@ -41,7 +41,7 @@ def test_dw_direct_rows_bitwise(dev, monkeypatch, R, FK, Fo):
     assert O.normwise_err(new.cpu().numpy(), ref.cpu().numpy()) < 1e-5
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["3", "2"])
 @pytest.mark.parametrize("R,Fin,K,Fo", [(200001, 64, 3, 64), (102400, 32, 20, 32), (80000, 16, 5, 128)])
 def test_dw_direct_planes_bitwise(dev, monkeypatch, mode, R, Fin, K, Fo):
     from cnn_graph_amd import ops
@@ -77,7 +77,7 @@ def test_dw_direct_lstm_weight_grads_bitwise(dev, monkeypatch, R, Fin, K):
     hpl, xpl = hbuf[:R * H].view(R, H), xbuf[:R * Fin].view(R, Fin)
     monkeypatch.setenv("CG_DW_DIRECT", "0")
     old = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
-    monkeypatch.setenv("CG_DW_DIRECT", "1")
+    monkeypatch.setenv("CG_DW_DIRECT", "3")  # forced, whatever the wave count
     new = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
     torch.cuda.synchronize()
     for a, b in zip(new, old):
