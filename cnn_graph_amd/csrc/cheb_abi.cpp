@@ -66,6 +66,11 @@ struct cg_plan {
   int* seq_fault_dev = nullptr;  // its device alias
   hipEvent_t seq_event = nullptr;
   bool seq_launched = false;
+  // side stream of the backward: dW (basis^T dy) runs on it concurrently with
+  // the dx recurrence, which does not read dW (fork / join by events, so it
+  // also works under stream capture); created on first use
+  hipStream_t side = nullptr;
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
 };
 
 namespace {
@@ -285,7 +290,27 @@ void free_plan(cg_plan* p) {
   if (p->tfast.buf) (void)hipFree(p->tfast.buf);
   if (p->seq_event) (void)hipEventDestroy(p->seq_event);
   if (p->seq_fault) (void)hipHostFree(p->seq_fault);
+  if (p->side_fork) (void)hipEventDestroy(p->side_fork);
+  if (p->side_join) (void)hipEventDestroy(p->side_join);
+  if (p->side) (void)hipStreamDestroy(p->side);
   delete p;
+}
+
+// CG_SIDE_DW: 0 = dW in stream order after dx; 1 (default) = dW on the plan's
+// side stream where the dx kernel leaves CUs idle (the channel-group
+// recurrence: config R's 400 workgroups of one per CU run in two rounds, the
+// second 56 % full); 2 = on every non-fused path (A/B runs).  Read per call.
+int side_dw_mode() {
+  const char* e = getenv("CG_SIDE_DW");
+  return (e && e[0]) ? atoi(e) : 1;
+}
+
+int side_ready(cg_plan* p) {
+  if (p->side) return CG_OK;
+  CG_HIP(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+  CG_HIP(hipEventCreateWithFlags(&p->side_fork, hipEventDisableTiming));
+  CG_HIP(hipEventCreateWithFlags(&p->side_join, hipEventDisableTiming));
+  return CG_OK;
 }
 
 int check_device(const cg_plan* p) {
@@ -854,9 +879,10 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   const int64_t R = int64_t(N) * M;
   const int chunks = cg::dw_chunks(R);
 
-  // Everything runs on the caller's stream.  (Forking the streaming dW GEMM
-  // onto a side stream to overlap the dx recurrence was measured on MI355X:
-  // the event fork + join costs ~20 us per call, more than the overlap gains.)
+  // Everything runs on the caller's stream except the channel-group path's dW
+  // (side_dw_mode).  (Forking the streaming dW GEMM onto a side stream to
+  // overlap the dx recurrence was measured on MI355X in round 1: the event
+  // fork + join costs ~20 us per call, more than the overlap gains there.)
   char* base = static_cast<char*>(workspace);
   float* slabs = reinterpret_cast<float*>(base);
   const bool dypass = path != CG_PATH_RESIDENT && stream_ws(plan, N, Fin, K, Fout).wide &&
@@ -865,6 +891,13 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   const bool fused =
       dx != nullptr && dW != nullptr && path == CG_PATH_RESIDENT && fused_dw(plan, Fin, K, Fout);
   int nslab_ready = 0;  // dW slabs a kernel of the dx pass already wrote
+  bool dw_done = false;  // dW slabs launched on the side stream
+  auto launch_dw = [&](hipStream_t st) -> hipError_t {
+    if (cg::debug_flags() & (1 << 22)) return hipSuccess;  // ablation hook (debug build): skip dW
+    return cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, st,
+                               layout == CG_BASIS_PLANES ? Fin : 0,
+                               layout == CG_BASIS_PLANES ? int64_t(R) * Fin : 0, K);
+  };
   if (dx) {
     if (path == CG_PATH_RESIDENT && use_fast(plan, Fin, K, Fout, true)) {
       const cg::FastGeom g = fast_geom(plan, Fin, K, Fout);
@@ -927,9 +960,23 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
     } else if (!stream_ws(plan, N, Fin, K, Fout).wide && use_group(plan, Fin, K, Fout) &&
                cg::grp_clen_dy_ok(M, plan->nnzT, K, Fout)) {
       // the whole reverse recurrence in LDS per (sample, 8 channels), dBasis
-      // formed in the kernel from dy and W (no dBasis planes)
+      // formed in the kernel from dy and W (no dBasis planes); dW on the side
+      // stream, into the CUs the recurrence's second round leaves idle
+      const bool side = dW && side_dw_mode() >= 1;
+      if (side) {
+        const int rc = side_ready(plan);
+        if (rc) return rc;
+        CG_HIP(hipEventRecord(plan->side_fork, s));
+      }
       CG_HIP(cg::launch_grp_clen_dy(plan->trowptr, plan->tcol, plan->tval, plan->tlorder, plan->nnzT,
                                     N, M, Fin, K, Fout, dy, W, dx, dx_acc, s));
+      if (side) {
+        CG_HIP(hipStreamWaitEvent(plan->side, plan->side_fork, 0));
+        CG_HIP(launch_dw(plan->side));
+        CG_HIP(hipEventRecord(plan->side_join, plan->side));
+        CG_HIP(hipStreamWaitEvent(s, plan->side_join, 0));
+        dw_done = true;
+      }
     } else {
       float* dA = reinterpret_cast<float*>(rest);
       const int NM = N * M;
@@ -983,10 +1030,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   }
   if (!dW) return ok();
   if (fused) nslab_ready = N;
-  if (!nslab_ready && !(cg::debug_flags() & (1 << 22)))  // ablation hook (debug build): skip dW
-    CG_HIP(cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, s,
-                               layout == CG_BASIS_PLANES ? Fin : 0,
-                               layout == CG_BASIS_PLANES ? int64_t(R) * Fin : 0, K));
+  if (!nslab_ready && !dw_done) CG_HIP(launch_dw(s));
   const int nslab = nslab_ready ? nslab_ready : chunks;
   if (adam)  // reduction + optimizer step in one launch (no exchange in between)
     CG_HIP(cg::launch_reduce_slabs_adam(slabs, nslab, int64_t(FinK) * Fout, dW, *adam, s));

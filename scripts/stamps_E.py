@@ -6,8 +6,9 @@ every pair: 0 step start, 1 own quarters' recurrence done (seq2: phase 1),
 3 all quarters contracted, 4 epilogue done].  Median over workgroups, us from
 the step start; plus the HIP-event time of the layer forward.  An optional
 argument sets the debug build's ablation flags for the whole run (k_lstm_seq2
-phase 2: 1 no MFMA, 4 linear gates, 16 no gx / c loads, 64 no act stores,
-128 no c stores, 256 no h stores; outputs are garbage, times only).
+phase 2: 1 no MFMA, 2 no SpMM, 4 linear gates, 16 no gx / c loads, 64 no
+act stores, 128 no c stores; outputs are garbage, times only); they go to the
+sequence kernels' byte of the debug flags (bits 16-23).
   python3 scripts/stamps_E.py [FLAGS]"""
 import ctypes
 import json
@@ -53,7 +54,7 @@ def main():
     h.cg_debug_set_ts.argtypes = [ctypes.c_void_p]
     flags = int(sys.argv[1]) if len(sys.argv) > 1 else 0
     h.cg_debug_set_flags.argtypes = [ctypes.c_int]
-    h.cg_debug_set_flags(flags)
+    h.cg_debug_set_flags(flags << 16)
     for _ in range(3):
         run()
     torch.cuda.synchronize()

@@ -126,3 +126,37 @@ def test_group_clenshaw_packed_columns_bitwise(dev, monkeypatch, gname, N, Fin, 
         out[name] = r.dx.clone()
     assert torch.equal(out["pc"], out["lds"])
     assert torch.equal(out["pc"], out["steps"])
+
+
+@pytest.mark.parametrize("layout", ["rows", "planes"])
+def test_group_side_stream_dw_bitwise(dev, monkeypatch, layout):
+    """dW on the plan's side stream, concurrent with k_grp_clen_dy (default,
+    CG_SIDE_DW=1) against dW in stream order after it (CG_SIDE_DW=0): dx and
+    dW bitwise equal, and a read of dW right after the call on the caller's
+    stream sees the finished values (the join), over several back-to-back
+    calls that reuse the plan's fork / join events."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden("golden_E.npz"))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    N, Fin, K, Fout = 12, 32, 20, 32
+    rng = np.random.default_rng(77)
+    xt = _t(rng.standard_normal((N, M, Fin)), dev)
+    Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
+    dys = [_t(rng.standard_normal((N, M, Fout)), dev) for _ in range(3)]
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CG_SIDE_DW", mode)
+        plan = ChebPlan(Lt, device=0, path="stream")
+        r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=layout)
+        r.forward(xt, Wt)
+        res = []
+        for dy in dys:
+            r.backward(dy, Wt)
+            res.append((r.dx.clone(), r.dW.clone()))  # clones on the caller's stream
+        torch.cuda.synchronize()
+        out[mode] = res
+    for (dx0, dW0), (dx1, dW1) in zip(out["0"], out["1"]):
+        assert torch.equal(dx0, dx1)
+        assert torch.equal(dW0, dW1)
