@@ -296,13 +296,15 @@ void free_plan(cg_plan* p) {
   delete p;
 }
 
-// CG_SIDE_DW: 0 = dW in stream order after dx; 1 (default) = dW on the plan's
-// side stream where the dx kernel leaves CUs idle (the channel-group
-// recurrence: config R's 400 workgroups of one per CU run in two rounds, the
-// second 56 % full); 2 = on every non-fused path (A/B runs).  Read per call.
+// CG_SIDE_DW=1: dW on the plan's side stream, concurrent with the channel-group
+// recurrence k_grp_clen_dy (whose 400 workgroups of one per CU run in two
+// rounds on config R, the second 56 % full).  Off by default: measured 5.32
+// vs 4.90-4.92 ms per R step (profiles/r04_f) -- the dW workgroups take CUs as
+// the first round drains and the recurrence's second round starts up to 240
+// instead of 117 us into the call (phase stamps).  Read per call.
 int side_dw_mode() {
   const char* e = getenv("CG_SIDE_DW");
-  return (e && e[0]) ? atoi(e) : 1;
+  return (e && e[0]) ? atoi(e) : 0;
 }
 
 int side_ready(cg_plan* p) {
@@ -961,7 +963,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
                cg::grp_clen_dy_ok(M, plan->nnzT, K, Fout)) {
       // the whole reverse recurrence in LDS per (sample, 8 channels), dBasis
       // formed in the kernel from dy and W (no dBasis planes); dW on the side
-      // stream, into the CUs the recurrence's second round leaves idle
+      // stream with CG_SIDE_DW=1 (side_dw_mode)
       const bool side = dW && side_dw_mode() >= 1;
       if (side) {
         const int rc = side_ready(plan);

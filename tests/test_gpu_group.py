@@ -130,8 +130,8 @@ def test_group_clenshaw_packed_columns_bitwise(dev, monkeypatch, gname, N, Fin, 
 
 @pytest.mark.parametrize("layout", ["rows", "planes"])
 def test_group_side_stream_dw_bitwise(dev, monkeypatch, layout):
-    """dW on the plan's side stream, concurrent with k_grp_clen_dy (default,
-    CG_SIDE_DW=1) against dW in stream order after it (CG_SIDE_DW=0): dx and
+    """dW on the plan's side stream, concurrent with k_grp_clen_dy
+    (CG_SIDE_DW=1) against dW in stream order after it (default): dx and
     dW bitwise equal, and a read of dW right after the call on the caller's
     stream sees the finished values (the join), over several back-to-back
     calls that reuse the plan's fork / join events."""
