@@ -1077,8 +1077,8 @@ int dw_chunks(int64_t R) {
 // columns of the slice decide the B loads (VB, NLB), the basis columns (with
 // the LSTM's x-plane and ones columns) are cut into G groups of NA = VA*NLA
 // virtual tiles, NA chosen for the fewest MFMAs per row pair (G*NA*NB);
-// CG_DW_DIRECT=0 keeps k_dw_slabs (A/B runs), =2 prefers two-float basis loads,
-// =3 forces k_dw_direct whatever the wave count (tests; so does 2)
+// CG_DW_DIRECT=0 keeps k_dw_slabs (A/B runs); =2 forces k_dw_direct whatever
+// the wave count, =3 too but with one-float basis loads only (tests)
 static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
                              int ldd, float* slab, hipStream_t s, int pl_fin, int64_t pl_stride,
                              int K, int chunks, int64_t rpc, const float* xb, int x_fin,
@@ -1109,7 +1109,10 @@ static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int
   if (Fout <= 32) return go(k_dw_direct<1, 5, 1, 1, 12>, 5);
   if (!b2) return false;
   if (Fout <= 64) {
-    if (mode == 2 && a2) return go(k_dw_direct<2, 3, 2, 1, 8>, 6);
+    // two-float basis loads, six virtual tiles: FinK <= 192 in ONE column
+    // group, so dy is read once (config D: 17.5 ms per call against 19.7 for
+    // <1, 3, ...> and 20.6 for k_dw_slabs, profiles/r04_d)
+    if (a2 && mode != 3) return go(k_dw_direct<2, 3, 2, 1, 8>, 6);
     return go(k_dw_direct<1, 3, 2, 1, 12>, 3);
   }
   if (Fout <= 128) {

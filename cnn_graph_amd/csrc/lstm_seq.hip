@@ -320,6 +320,11 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
         const int Fin = A.Fin;
         for (int k = 0; k < K; ++k) {
           const float* xp = A.xplanes + int64_t(k) * A.xpstride + (int64_t(t) * N + n) * M * Fin;
+          // buffer loads: a padding row or a channel past Fin reads past the
+          // plane's range, which returns 0 -- no branch (a conditional load
+          // compiles to one with a vmcnt(0) wait behind every load)
+          const __amdgpu_buffer_rsrc_t rx =
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xp), 0, M * Fin * 4, 0x00020000);
           const float* wq = s_Wx + k * 512 + hh * 64 + j;
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
@@ -327,8 +332,10 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
             const int c = 2 * s + hh;
             float b[kRT];
 #pragma unroll
-            for (int rt = 0; rt < kRT; ++rt)
-              b[rt] = (rv[rt] && c < Fin) ? xp[int64_t(row[rt]) * Fin + c] : 0.f;
+            for (int rt = 0; rt < kRT; ++rt) {
+              const int xo = (rv[rt] && c < Fin) ? (row[rt] * Fin + c) * 4 : M * Fin * 4;
+              b[rt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, xo, 0, 0));
+            }
             const float a0 = wq[s * 128], a1 = wq[s * 128 + 32];
 #pragma unroll
             for (int rt = 0; rt < kRT; ++rt) {
@@ -494,6 +501,23 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
         }
       }
       if (stamp) CG_TS(A.ts, 3);
+      // c_{t-1} of every tile, loaded together before the first store of the
+      // epilogue (a load behind stores waits for them: vmcnt counts both):
+      // this lane's own store of the previous step (same address, same lane)
+      // or the initial state; buffer loads, a padding row (M) reads 0
+      float4 cva[kRT][2];
+      {
+        const float* csrc = t > 0 ? A.cs + (int64_t(t - 1) * N + n) * M * kH
+                                  : (A.c0 ? A.c0 + int64_t(n) * M * kH : A.cs);
+        const __amdgpu_buffer_rsrc_t r_c = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(csrc), 0, (t > 0 || A.c0) && !CG_DBG(A.dbg, 16) ? M * kH * 4 : 0,
+            0x00020000);
+#pragma unroll
+        for (int rt = 0; rt < kRT; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+            cva[rt][ct] = bld16(r_c, row[rt] * kH + 16 * u + 8 * ct + 4 * hh);
+      }
       // gate update: lane (row, hh) of tile (rt, ct) holds gates g = 0..3 of
       // units 16u + 8ct + 4hh + m in acc[rt][ct][4g + m]
 #pragma unroll
@@ -508,14 +532,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           for (int g = 0; g < 4; ++g)
             gv[g] = (CG_DBG(A.dbg, 16) || A.xs) ? make_float4(0.f, 0.f, 0.f, 0.f)
                                                 : *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
-          // c_{t-1}: this lane's own store of the previous step (same address,
-          // same lane), or the initial state
-          float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (CG_DBG(A.dbg, 16)) {
-          } else if (t > 0)
-            cv = *reinterpret_cast<const float4*>(A.cs + (rr - int64_t(N) * M) * kH + u0);
-          else if (A.c0)
-            cv = *reinterpret_cast<const float4*>(A.c0 + (int64_t(n) * M + row[rt]) * kH + u0);
+          const float4 cv = cva[rt][ct];
           float c[4] = {cv.x, cv.y, cv.z, cv.w};
           float hn[4], zz[4], ii[4], ff[4], oo[4];
 #pragma unroll
