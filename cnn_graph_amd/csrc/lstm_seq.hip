@@ -485,19 +485,26 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
         if (stamp) CG_TS(A.ts, 2);
         // the partner's two quarters: T_0 = its half of h_{t-1}, T_k its planes
         // (sc1 loads, no recurrence here: it computed them)
-        for (int qq = 0; qq < 2; ++qq) {
-          const int q = 2 * (1 - u) + qq;
-          for (int k = 0; k < K; ++k) {
-            const float* src = (k == 0) ? hsrc : pl_t + int64_t(k - 1) * A.pstride;
-            const __amdgpu_buffer_rsrc_t r_src = slab_rsrc(src, M);
-            float4 tk[kRT];
+        // items it = (qq, k), qq-major; item it + 1's loads are in flight
+        // during item it's MFMAs (two register sets, alternating)
+        auto ldq = [&](int it, float4 (&tk)[kRT]) {
+          const int q = 2 * (1 - u) + it / K, k = it % K;
+          const float* src = (k == 0) ? hsrc : pl_t + int64_t(k - 1) * A.pstride;
+          const __amdgpu_buffer_rsrc_t r_src = slab_rsrc(src, M);
 #pragma unroll
-            for (int rt = 0; rt < kRT; ++rt) {  // row M: past the slab, reads 0
-              const int off = row[rt] * kH + 8 * q + 4 * hh;
-              tk[rt] = (k == 0 && t == 0) ? bld16(r_src, off) : bld16_sc1(r_src, off);
-            }
-            contract(q, k, tk);
+          for (int rt = 0; rt < kRT; ++rt) {  // row M: past the slab, reads 0
+            const int off = row[rt] * kH + 8 * q + 4 * hh;
+            tk[rt] = (k == 0 && t == 0) ? bld16(r_src, off) : bld16_sc1(r_src, off);
           }
+        };
+        const int nit = 2 * K;
+        float4 tka[kRT], tkb[kRT];
+        ldq(0, tka);
+        for (int it = 0; it < nit; it += 2) {
+          ldq(it + 1, tkb);  // nit is even
+          contract(2 * (1 - u) + it / K, it % K, tka);
+          if (it + 2 < nit) ldq(it + 2, tka);
+          contract(2 * (1 - u) + (it + 1) / K, (it + 1) % K, tkb);
         }
       }
       if (stamp) CG_TS(A.ts, 3);
