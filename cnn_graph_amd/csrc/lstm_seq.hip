@@ -64,7 +64,6 @@ constexpr int kQ = 8;      // channels per forward SpMM pass (a quarter of H)
 constexpr int kBS = 16;    // channels per backward workgroup (half of H)
 constexpr int kRT = 4;     // forward: 32-row tiles per wave (8 waves x 4 x 32 = 1024 rows)
 constexpr int kRB = 8;     // backward: 16-row tiles per wave (8 x 8 x 16 = 1024 rows)
-constexpr int kActAhead = 4;  // backward: act pieces loaded one row tile ahead
 constexpr int kSeqStaticLds = 64;  // k_lstm_seq's static __shared__ bytes (upper bound)
 
 __device__ __forceinline__ float sigm(float a) { return 1.f / (1.f + expf(-a)); }
@@ -987,83 +986,50 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     for (int o = 0; o < K; ++o) acc[rt][o] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool ref = A.gates == 0;
   const bool own = (q >> 1) == u;  // this lane's units are stored by this workgroup
-  // phase A: dpre of units 8q .. 8q+7 of the lane's rows, and D_o.  Software
-  // pipelined over the row tiles: tile rt + 1's act loads are issued as soon
-  // as tile rt's pointwise math has consumed its registers, ahead of tile rt's
-  // stores (a load behind stores would wait for them: vmcnt counts both) and
-  // MFMAs.  The loads are buffer loads over one
-  // sample's slab: a padding row (M) or a NULL operand reads 0 through the
-  // descriptor's range check, so no load sits behind a branch.
-  const int64_t nb = int64_t(n) * M;
-  auto rsrc = [&](const float* base, int per_row) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base ? base + nb * per_row : base), 0,
-                                             base ? M * per_row * 4 : 0, 0x00020000);
-  };
-  const __amdgpu_buffer_rsrc_t r_act = rsrc(A.act, 128), r_cp = rsrc(A.c_prev, kH),
-                               r_co = rsrc(A.c_out, kH), r_dh = rsrc(A.dh, kH),
-                               r_dc = rsrc(A.dc, kH), r_dhr = rsrc(A.dh_rec, kH);
-  struct PhaseAIn {
-    float4 a[8];  // act: unit-major 8 records of 4 gates, or gate-major 4 x 8 units
-    float4 cp[2], co[2], dh[2], dc[2], dhr[2];
-  };
-  // the first kActAhead 16-byte pieces of the act record (128 of the 168
-  // bytes a lane reads per row) go one tile ahead, the rest and the state
-  // vectors are loaded at the tile's start (more in flight spills at 256
-  // registers)
-  // act record pieces e0 .. e1-1 (16 bytes each) of tile rt
-  auto ldact = [&](int rt, PhaseAIn& v, int e0, int e1) {
-    const int row = rows[rt];  // M: past the slab
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (e < e0 || e >= e1) continue;
-      v.a[e] = A.act_um ? bld16(r_act, row * 128 + 32 * q + 4 * e)
-                        : bld16(r_act, row * 128 + (e >> 1) * 32 + 8 * q + 4 * (e & 1));
-    }
-  };
-  auto ldstate = [&](int rt, PhaseAIn& v) {
-    const int hb = rows[rt] * kH + 8 * q;
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      v.cp[h2] = bld16(r_cp, hb + 4 * h2);
-      v.co[h2] = bld16(r_co, hb + 4 * h2);
-      v.dh[h2] = bld16(r_dh, hb + 4 * h2);
-      v.dc[h2] = bld16(r_dc, hb + 4 * h2);
-      v.dhr[h2] = bld16(r_dhr, hb + 4 * h2);
-    }
-  };
-  PhaseAIn in;
-  if (!CG_DBG(A.dbg, 2)) ldact(0, in, 0, kActAhead);
+  // phase A: dpre of units 8q .. 8q+7 of the lane's rows, and D_o
 #pragma unroll
   for (int rt = 0; rt < kRB; ++rt) {
     const int row = rows[rt];
-    const bool live = row < M && !CG_DBG(A.dbg, 2);
-    float dp[4][8], dcp[8];
-    if (!CG_DBG(A.dbg, 2)) {
-      ldact(rt, in, kActAhead, 8);
-      ldstate(rt, in);
-      float av[4][8], cp[8], co[8], dhv[8], dcv[8], dhr[8];
-      if (A.act_um) {
+    float dp[4][8];
+    if (row < M && !CG_DBG(A.dbg, 2)) {
+      const int64_t rr = int64_t(n) * M + row;
+      const int64_t hb = rr * kH + 8 * q;
+      float av[4][8], cp[8], co[8], dhv[8], dcv[8];
+      if (A.act_um) {  // units 8q .. 8q+7: one contiguous 128-byte record
+        const float* ap = A.act + rr * 128 + 32 * q;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-          av[0][m] = in.a[m].x; av[1][m] = in.a[m].y; av[2][m] = in.a[m].z; av[3][m] = in.a[m].w;
+          const float4 x = *reinterpret_cast<const float4*>(ap + 4 * m);
+          av[0][m] = x.x; av[1][m] = x.y; av[2][m] = x.z; av[3][m] = x.w;
         }
       } else {
+        const float* ap = A.act + rr * 128 + 8 * q;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float4 x0 = in.a[2 * g], x1 = in.a[2 * g + 1];
+          const float4 x0 = *reinterpret_cast<const float4*>(ap + g * 32);
+          const float4 x1 = *reinterpret_cast<const float4*>(ap + g * 32 + 4);
           av[g][0] = x0.x; av[g][1] = x0.y; av[g][2] = x0.z; av[g][3] = x0.w;
           av[g][4] = x1.x; av[g][5] = x1.y; av[g][6] = x1.z; av[g][7] = x1.w;
         }
       }
-      auto un = [](const float4 (&v)[2], float* o) {
-        o[0] = v[0].x; o[1] = v[0].y; o[2] = v[0].z; o[3] = v[0].w;
-        o[4] = v[1].x; o[5] = v[1].y; o[6] = v[1].z; o[7] = v[1].w;
+      auto ld8 = [&](const float* base, float* out) {
+        if (base) {
+          const float4 x0 = *reinterpret_cast<const float4*>(base + hb);
+          const float4 x1 = *reinterpret_cast<const float4*>(base + hb + 4);
+          out[0] = x0.x; out[1] = x0.y; out[2] = x0.z; out[3] = x0.w;
+          out[4] = x1.x; out[5] = x1.y; out[6] = x1.z; out[7] = x1.w;
+        } else {
+#pragma unroll
+          for (int m = 0; m < 8; ++m) out[m] = 0.f;
+        }
       };
-      un(in.cp, cp);
-      un(in.co, co);
-      un(in.dh, dhv);
-      un(in.dc, dcv);
-      un(in.dhr, dhr);
+      ld8(A.c_prev, cp);
+      ld8(A.c_out, co);
+      ld8(A.dh, dhv);
+      ld8(A.dc, dcv);
+      float dhr[8];
+      ld8(A.dh_rec, dhr);
+      float dcp[8];
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         // the expressions (and their order) of lstm.hip::k_lstm_bwd
@@ -1081,16 +1047,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
         dp[3][m] = ref ? d_o * (1.f - o * o) : d_o * (o * (1.f - o));
         dcp[m] = dcn * f;
       }
-      if (rt + 1 < kRB) ldact(rt + 1, in, 0, kActAhead);  // consumed: the next tile's fly
-      if (!live) {  // a padding row contributes zeros to D
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int m = 0; m < 8; ++m) dp[g][m] = 0.f;
-      }
-      if (own && live) {
-        const int64_t rr = nb + row;
-        const int64_t hb = rr * kH + 8 * q;
+      if (own) {
         float* dq = A.dpre + rr * 128 + 8 * q;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
