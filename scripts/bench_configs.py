@@ -13,7 +13,7 @@ rounds; alg_GBps uses SURVEY.md §8d's algorithmic bytes.  Each line carries a
 `cpu_baseline`: the oracle's fwd+bwd of the same config on the host cores
 (bench.py's CPU legs -- the only place outside tests/ that runs oracle/),
 median of the timed passes, with the sub-batch and pass count stated.
-Usage: python scripts/bench_configs.py [C1 C2 D E R] [--d-batch N] [--layout rows|planes]
+Usage: python scripts/bench_configs.py [C1 C2 D E R] [--d-batch N] [--layout auto|rows|planes]
                                        [--no-cpu] [--cpu-seconds S]
 """
 from __future__ import annotations
@@ -58,7 +58,7 @@ def alg_bytes(M, nnz, B, K):
     return (K - 1) * csr + 4 * M * B * (2 + 3 * (K - 2)), (K - 1) * csr + 4 * M * B * (3 + 5 * (K - 2))
 
 
-def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="rows"):
+def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="auto"):
     M = Lt.shape[0]
     plan = ChebPlan(Lt, device=0, variant=variant)
     g = torch.Generator(device=dev)
@@ -66,6 +66,8 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="rows")
     x = torch.rand((N, M, Fin), device=dev, generator=g)
     W = torch.randn((Fin * K, Fout), device=dev, generator=g) * 0.1
     dy = torch.randn((N, M, Fout), device=dev, generator=g)
+    if layout == "auto":  # what the autograd layers use (ops.basis_layout_for)
+        layout = ops.basis_layout_for(plan, N, Fin, K, Fout)
     if layout != "rows" and plan.basis_elems(N, Fin, K, Fout, layout) is None:
         return None  # the layout does not apply to this shape
     r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=layout)
@@ -153,8 +155,9 @@ def main():
     ap.add_argument("configs", nargs="*", default=["C1", "C2", "D", "E"])
     ap.add_argument("--d-batch", type=int, default=32)
     ap.add_argument("--variant", default="auto", help="plan variant (auto / narrow / ...)")
-    ap.add_argument("--layout", default="rows", choices=["rows", "planes"],
-                    help="basis layout of the C1/C2/D filters (planes: where it applies)")
+    ap.add_argument("--layout", default="auto", choices=["auto", "rows", "planes"],
+                    help="basis layout of the C1/C2/D filters (auto: the autograd layers' choice, "
+                         "ops.basis_layout_for -- planes where it applies, else rows)")
     ap.add_argument("--rounds", type=int, default=3, help="timed rounds per measurement (median)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
