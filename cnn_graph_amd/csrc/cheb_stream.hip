@@ -747,7 +747,7 @@ template <int V> __device__ __forceinline__ float dw_el(const typename DwVec<V>:
 }
 
 template <int VA, int NLA, int VB, int NLB, int PD>
-__global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
+__device__ __forceinline__ void dw_direct_body(const DwDirectArgs& A) {
   typedef typename DwVec<VA>::T TA;
   typedef typename DwVec<VB>::T TB;
   constexpr int NA = VA * NLA, NB = VB * NLB;
@@ -873,6 +873,18 @@ __global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
           A.slab[(int64_t(chunk) * FinK + jo) * A.ldd + f] = acc[a][b][r];
       }
     }
+}
+
+// one wave per SIMD (up to 512 registers: the deep rings / wide tile sets)
+template <int VA, int NLA, int VB, int NLB, int PD>
+__global__ __launch_bounds__(256) void k_dw_direct(DwDirectArgs A) {
+  dw_direct_body<VA, NLA, VB, NLB, PD>(A);
+}
+// two waves per SIMD (<= 256 registers): one wave's loads run under the
+// other's MFMAs, for the instantiations that fit without spills
+template <int VA, int NLA, int VB, int NLB, int PD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_dw_direct2(DwDirectArgs A) {
+  dw_direct_body<VA, NLA, VB, NLB, PD>(A);
 }
 
 // out[i] = sum_z slab[z][i] in a FIXED order (bitwise reproducible): wave w of
@@ -1073,6 +1085,13 @@ int dw_chunks(int64_t R) {
   return int(c < 1 ? 1 : c);
 }
 
+// CG_DW_W2=1: the two-waves-per-SIMD build of the instantiations that fit in
+// 256 registers (A/B runs); read per call
+static bool dw_two_waves() {
+  const char* e = getenv("CG_DW_W2");
+  return e && e[0] == '1';
+}
+
 // k_dw_direct for this shape, if one of its instantiations serves it: the dy
 // columns of the slice decide the B loads (VB, NLB), the basis columns (with
 // the LSTM's x-plane and ones columns) are cut into G groups of NA = VA*NLA
@@ -1106,20 +1125,22 @@ static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int
     return true;
   };
   auto mfmas = [&](int na) { return (FinK + 32 * na - 1) / (32 * na) * na; };  // per B tile
-  if (Fout <= 32) return go(k_dw_direct<1, 5, 1, 1, 12>, 5);
+  const bool w2 = dw_two_waves();
+  if (Fout <= 32) return w2 ? go(k_dw_direct2<1, 5, 1, 1, 12>, 5) : go(k_dw_direct<1, 5, 1, 1, 12>, 5);
   if (!b2) return false;
   if (Fout <= 64) {
     // two-float basis loads, six virtual tiles: FinK <= 192 in ONE column
     // group, so dy is read once (config D: 17.5 ms per call against 19.7 for
     // <1, 3, ...> and 20.6 for k_dw_slabs, profiles/r04_d)
     if (a2 && mode != 3) return go(k_dw_direct<2, 3, 2, 1, 8>, 6);
-    return go(k_dw_direct<1, 3, 2, 1, 12>, 3);
+    return w2 ? go(k_dw_direct2<1, 3, 2, 1, 12>, 3) : go(k_dw_direct<1, 3, 2, 1, 12>, 3);
   }
   if (Fout <= 128) {
-    if (mfmas(2) < mfmas(3)) return go(k_dw_direct<1, 2, 2, 2, 10>, 2);
+    if (mfmas(2) < mfmas(3))
+      return w2 ? go(k_dw_direct2<1, 2, 2, 2, 10>, 2) : go(k_dw_direct<1, 2, 2, 2, 10>, 2);
     return go(k_dw_direct<1, 3, 2, 2, 8>, 3);
   }
-  return go(k_dw_direct<1, 1, 2, 4, 8>, 1);
+  return w2 ? go(k_dw_direct2<1, 1, 2, 4, 8>, 1) : go(k_dw_direct<1, 1, 2, 4, 8>, 1);
 }
 
 static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int64_t R, int FinKh,

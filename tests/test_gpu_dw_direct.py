@@ -83,3 +83,48 @@ def test_dw_direct_lstm_weight_grads_bitwise(dev, monkeypatch, R, Fin, K):
     for a, b in zip(new, old):
         assert torch.equal(a, b)
     assert O.normwise_err(new[2].cpu().numpy(), dpre.double().sum(0).cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("R,FK,Fo", [(300001, 160, 32), (200003, 192, 64), (131072, 96, 128),
+                                     (140001, 40, 256)])
+def test_dw_direct_two_waves_bitwise(dev, monkeypatch, R, FK, Fo):
+    """The two-waves-per-SIMD build (CG_DW_W2=1, <= 256 registers) against the
+    one-wave build and k_dw_slabs: dW bitwise equal (same chunks, same pairs,
+    same MFMA sequence per output)."""
+    from cnn_graph_amd import ops
+    g = torch.Generator(device=dev)
+    g.manual_seed(R + 7 * FK + Fo)
+    A = torch.randn((R, FK), device=dev, generator=g)
+    D = torch.randn((R, Fo), device=dev, generator=g)
+    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    ref = ops.weight_grad(A, D)
+    out = {}
+    for w2 in ("0", "1"):
+        monkeypatch.setenv("CG_DW_DIRECT", "3")
+        monkeypatch.setenv("CG_DW_W2", w2)
+        out[w2] = ops.weight_grad(A, D)
+    torch.cuda.synchronize()
+    assert torch.equal(out["0"], ref)
+    assert torch.equal(out["1"], ref)
+
+
+def test_dw_direct_two_waves_lstm_bitwise(dev, monkeypatch):
+    """cg_lstm_weight_grads (config E's shape class: H 32, Fin 2, K 3) on the
+    two-waves build: dWh, dWx, db bitwise the one-wave build's."""
+    from cnn_graph_amd import ops
+    R, H, Fin, K = 12 * 8 * 1024, 32, 2, 3
+    g = torch.Generator(device=dev)
+    g.manual_seed(99)
+    hst, xst = R * H + 96, R * Fin + 40
+    hbuf = torch.randn((K * hst,), device=dev, generator=g)
+    xbuf = torch.randn((K * xst,), device=dev, generator=g)
+    dpre = torch.randn((R, 4 * H), device=dev, generator=g)
+    hpl, xpl = hbuf[:R * H].view(R, H), xbuf[:R * Fin].view(R, Fin)
+    out = {}
+    for w2 in ("0", "1"):
+        monkeypatch.setenv("CG_DW_DIRECT", "3")
+        monkeypatch.setenv("CG_DW_W2", w2)
+        out[w2] = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
+    torch.cuda.synchronize()
+    for a, b in zip(out["0"], out["1"]):
+        assert torch.equal(a, b)
