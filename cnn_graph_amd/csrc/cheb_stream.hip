@@ -1085,11 +1085,13 @@ int dw_chunks(int64_t R) {
   return int(c < 1 ? 1 : c);
 }
 
-// CG_DW_W2=1: the two-waves-per-SIMD build of the instantiations that fit in
-// 256 registers (A/B runs); read per call
+// the two-waves-per-SIMD build of the instantiations that fit in 256
+// registers: config C2's dW 223 -> 215 us, config E's weight-gradient pass
+// 584 -> 551 us (profiles/r04_j).  CG_DW_W2=0 keeps the one-wave build (A/B);
+// read per call
 static bool dw_two_waves() {
   const char* e = getenv("CG_DW_W2");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }
 
 // k_dw_direct for this shape, if one of its instantiations serves it: the dy

@@ -13,7 +13,7 @@ rounds; alg_GBps uses SURVEY.md §8d's algorithmic bytes.  Each line carries a
 `cpu_baseline`: the oracle's fwd+bwd of the same config on the host cores
 (bench.py's CPU legs -- the only place outside tests/ that runs oracle/),
 median of the timed passes, with the sub-batch and pass count stated.
-Usage: python scripts/bench_configs.py [C1 C2 D E R] [--d-batch N] [--layout auto|rows|planes]
+Usage: python scripts/bench_configs.py [A C1 C2 D E R] [--d-batch N] [--layout auto|rows|planes]
                                        [--no-cpu] [--cpu-seconds S]
 """
 from __future__ import annotations
@@ -169,7 +169,14 @@ def main():
     from cnn_graph_amd.graph import rescale_L
     for name in args.configs:
         cpu = None
-        if name in ("C1", "C2"):
+        if name == "A":  # the usage recipe's 4-NN graph, M = 100
+            with np.load(os.path.join(ROOT, "tests", "golden", "golden_A.npz"), allow_pickle=False) as z:
+                M = int(z["M"])
+                Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
+            out = filter_config("A", Lt, 32, 1, 5, 4, dev, args.variant, args.layout)
+            cpu = lambda: bench.cpu_baseline_filter("A", Lt, 32, 32, 1, 5, 4,  # noqa: E731
+                                                    seconds=args.cpu_seconds)
+        elif name in ("C1", "C2"):
             with np.load(os.path.join(ROOT, "tests", "golden", "golden_C.npz"), allow_pickle=False) as z:
                 M = int(z["M"])
                 Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
