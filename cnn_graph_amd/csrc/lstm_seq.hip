@@ -689,9 +689,6 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
   }
   __syncthreads();
   constexpr int NP = 6;  // packed columns: rows of up to 12 entries (longer: LDS columns)
-  unsigned pk[kRT][NP];
-#pragma unroll
-  for (int rt = 0; rt < kRT; ++rt) pack_row_cols<NP>(pk[rt], s_col, rb[rt], re[rt], M);
 
   int* my_flag = A.flags + 2 * pair + u;
   const int* partner_flag = A.flags + 2 * pair + (1 - u);
@@ -707,7 +704,15 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
       const __amdgpu_buffer_rsrc_t r_hsrc = slab_rsrc(hsrc, M);
       const __amdgpu_buffer_rsrc_t r_hout = slab_rsrc(A.hs + (int64_t(t) * N + n) * M * kH, M);
       if (has_h) {
-        // phase 1: the recurrence of the OWN two quarters (units 16u .. 16u+15)
+        // phase 1: the recurrence of the OWN two quarters (units 16u .. 16u+15).
+        // The rows' CSR columns are packed into registers anew every step (a
+        // few LDS reads): held across phase 2 they would cost it 24 registers;
+        // the empty asm keeps the compiler from hoisting the packing out of
+        // the loop
+        asm volatile("" ::: "memory");
+        unsigned pk[kRT][NP];
+#pragma unroll
+        for (int rt = 0; rt < kRT; ++rt) pack_row_cols<NP>(pk[rt], s_col, rb[rt], re[rt], M);
         for (int qq = 0; qq < 2; ++qq) {
           const int q = 2 * u + qq;
           float4 v[kRT];
@@ -780,30 +785,77 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
         }
       }
       if (stamp) CG_TS(A.ts, 2);
-      // phase 2: per tile, all quarters' T_k from L2 -> MFMA -> gates -> stores
-      const float* xp = XPRE ? A.xplanes + (int64_t(t) * N + n) * M * A.Fin : nullptr;
-      auto load_tile = [&](int rt, float4 (&tk)[4][KK]) {
+      // phase 2: per tile, all quarters' T_k from L2 -> MFMA -> gates -> stores.
+      // (a) this step's x basis values staged in slot0 as [row][k Fin + c]
+      // (phase 1 is done with the slots; rows past the graph read the zero
+      // row M), so no tile waits on a global x load
+      if (XPRE) {
+        const int Fin = A.Fin, MF = M * Fin;
+        const float* xp = A.xplanes + (int64_t(t) * N + n) * M * Fin;
+        stage_lds<8, kST>(K * MF, [&](int e) {
+          const int k = e / MF;
+          return xp[int64_t(k) * A.xpstride + (e - k * MF)];
+        }, [&](int e, float v) {
+          const int k = e / MF, rem = e - k * MF, row = rem / Fin;
+          slot0[row * kQ + k * Fin + (rem - row * Fin)] = v;
+        });
+        __syncthreads();
+      }
+      // (b) per tile: T_k of the four quarters and c_{t-1} loaded one tile ahead
+      // (buffer loads, a padding row reads 0); the weight operands of the next
+      // (quarter, order) group read from LDS ahead of the current group's MFMAs
+      const float* csrc = t > 0 ? A.cs + (int64_t(t - 1) * N + n) * M * kH
+                                : (A.c0 ? A.c0 + int64_t(n) * M * kH : A.cs);
+      const __amdgpu_buffer_rsrc_t r_c = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(csrc), 0, (t > 0 || A.c0) && !CG_DBG(A.dbg, 16) ? M * kH * 4 : 0,
+          0x00020000);
+      // the tile's graph row of this lane, M (the zero row) past the graph
+      auto row_n = [&](int rt) {
+        const int r = (4 * wave + rt) * 32 + j;
+        return r < M ? r : M;
+      };
+      struct TileOps {
+        float4 tk[4][KK];
+        float4 cv[2];
+      };
+      auto load_tile = [&](int rt, TileOps& o) {
 #pragma unroll
         for (int qi = 0; qi < 4; ++qi) {
           const int q = qi < 2 ? 2 * u + qi : 2 * (1 - u) + (qi - 2);
 #pragma unroll
           for (int k = 0; k < KK; ++k) {
             if (!has_h) continue;
-            const int off = rN[rt] * kH + 8 * q + 4 * hh;
+            const int off = row_n(rt) * kH + 8 * q + 4 * hh;
             if (k == 0)
-              tk[qi][k] = t > 0 ? bld16_sc1(r_hsrc, off) : bld16(r_hsrc, off);
+              o.tk[qi][k] = t > 0 ? bld16_sc1(r_hsrc, off) : bld16(r_hsrc, off);
             else
-              tk[qi][k] = bld16_sc1(slab_rsrc(pl_t + int64_t(k - 1) * A.pstride, M), off);
+              o.tk[qi][k] = bld16_sc1(slab_rsrc(pl_t + int64_t(k - 1) * A.pstride, M), off);
           }
         }
-      };
-      float4 tkb[PF ? 2 : 1][4][KK];
-      load_tile(0, tkb[0]);
 #pragma unroll
+        for (int ct = 0; ct < 2; ++ct) o.cv[ct] = bld16(r_c, row_n(rt) * kH + 16 * u + 8 * ct + 4 * hh);
+      };
+      // weight operands of group g = qi * KK + k: (s, ct) -> wq[s * 128 + ct * 32]
+      auto load_w = [&](int g, float (&w)[8]) {
+        const int qi = g / KK, k = g - qi * KK;
+        const int q = qi < 2 ? 2 * u + qi : 2 * (1 - u) + (qi - 2);
+        const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          w[2 * s] = wq[s * 128];
+          w[2 * s + 1] = wq[s * 128 + 32];
+        }
+      };
+      TileOps tob[PF ? 2 : 1];
+      load_tile(0, tob[0]);
+      // PF: unrolled, the next tile's loads in flight; else a real loop (one
+      // tile's registers live at a time)
+#pragma unroll(PF ? kRT : 1)
       for (int rt = 0; rt < kRT; ++rt) {
-        float4 (&tk)[4][KK] = tkb[PF ? (rt & 1) : 0];
-        if (PF && rt + 1 < kRT) load_tile(rt + 1, tkb[PF ? ((rt + 1) & 1) : 0]);  // in flight now
-        else if (!PF && rt > 0) load_tile(rt, tkb[0]);
+        TileOps& to = tob[PF ? (rt & 1) : 0];
+        float4 (&tk)[4][KK] = to.tk;
+        if (PF && rt + 1 < kRT) load_tile(rt + 1, tob[PF ? ((rt + 1) & 1) : 0]);  // in flight now
+        else if (!PF && rt > 0) load_tile(rt, tob[0]);
         f32x16 acc[2];
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct)
@@ -811,39 +863,41 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
           for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
         if (XPRE) {
           const int Fin = A.Fin;
-          for (int k = 0; k < K; ++k) {
-            const float* xk = xp + int64_t(k) * A.xpstride;
+#pragma unroll
+          for (int k = 0; k < KK; ++k) {
             const float* wq = s_Wx + k * 512 + hh * 64 + j;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
               if (2 * s >= Fin || CG_DBG(A.dbg, 1)) break;
               const int c = 2 * s + hh;
-              const float b = (rv[rt] && c < Fin) ? xk[int64_t(rN[rt]) * Fin + c] : 0.f;
+              const float xv = slot0[row_n(rt) * kQ + k * Fin + (c < Fin ? c : 0)];
+              const float b = c < Fin ? xv : 0.f;
               acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wq[s * 128], b, acc[0], 0, 0, 0);
               acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wq[s * 128 + 32], b, acc[1], 0, 0, 0);
             }
           }
         }
         if (has_h && !CG_DBG(A.dbg, 1)) {
+          float w[2][8];
+          load_w(0, w[0]);
 #pragma unroll
-          for (int qi = 0; qi < 4; ++qi) {
-            const int q = qi < 2 ? 2 * u + qi : 2 * (1 - u) + (qi - 2);
+          for (int g = 0; g < 4 * KK; ++g) {
+            if (g + 1 < 4 * KK) load_w(g + 1, w[(g + 1) & 1]);
+            const int qi = g / KK, k = g - qi * KK;
 #pragma unroll
-            for (int k = 0; k < KK; ++k) {
-              const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
-#pragma unroll
-              for (int s = 0; s < 4; ++s) {
-                const float b = (&tk[qi][k].x)[s];
-                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wq[s * 128], b, acc[0], 0, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wq[s * 128 + 32], b, acc[1], 0, 0, 0);
-              }
+            for (int s = 0; s < 4; ++s) {
+              const float b = (&tk[qi][k].x)[s];
+              acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[g & 1][2 * s], b, acc[0], 0, 0, 0);
+              acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[g & 1][2 * s + 1], b, acc[1], 0, 0, 0);
             }
+            // the scheduler would otherwise hoist every group's weight reads
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
         // gate update of this tile: lane (row, hh) of tile ct holds gates g = 0..3
         // of units 16u + 8ct + 4hh + m in acc[ct][4g + m]
-        if (!rv[rt]) continue;
-        const int64_t rr = (int64_t(t) * N + n) * M + rN[rt];
+        if (row_n(rt) >= M) continue;
+        const int64_t rr = (int64_t(t) * N + n) * M + row_n(rt);
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
           const int u0 = 16 * u + 8 * ct + 4 * hh;
@@ -852,12 +906,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
           for (int g = 0; g < 4; ++g)
             gv[g] = (CG_DBG(A.dbg, 16) || A.xs) ? make_float4(0.f, 0.f, 0.f, 0.f)
                                                 : *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
-          float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (CG_DBG(A.dbg, 16)) {
-          } else if (t > 0)
-            cv = *reinterpret_cast<const float4*>(A.cs + (rr - int64_t(N) * M) * kH + u0);
-          else if (A.c0)
-            cv = *reinterpret_cast<const float4*>(A.c0 + (int64_t(n) * M + rN[rt]) * kH + u0);
+          const float4 cv = to.cv[ct];
           float c[4] = {cv.x, cv.y, cv.z, cv.w};
           float hn[4], zz[4], ii[4], ff[4], oo[4];
 #pragma unroll
@@ -898,7 +947,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
           if (!CG_DBG(A.dbg, 128))
             *reinterpret_cast<float4*>(A.cs + rr * kH + u0) = make_float4(c[0], c[1], c[2], c[3]);
           if (!CG_DBG(A.dbg, 256))
-            bst16_sc1(r_hout, rN[rt] * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
+            bst16_sc1(r_hout, row_n(rt) * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
           if (A.act && !CG_DBG(A.dbg, 64)) {
             float* ap = A.act + rr * 128 + 4 * u0;
 #pragma unroll
@@ -908,8 +957,9 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
         }
       }
       if (stamp) CG_TS(A.ts, 3);
-      // the next step's phase 1 reloads h with the lanes that stored it; its
-      // LDS slots are free (phase 2 reads none), so no barrier is needed here
+      // the next step's phase 1 reloads h into slot0, which holds this step's
+      // x values until every wave's phase 2 is done
+      if (XPRE) __syncthreads();
     }
   }
 }
@@ -1247,7 +1297,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   else if (K == 1)
     kern = reinterpret_cast<const void*>(&k_lstm_seq2<true, 1, true>);
   else
-    kern = reinterpret_cast<const void*>(&k_lstm_seq2<true, 3, true>);
+    kern = reinterpret_cast<const void*>(&k_lstm_seq2<true, 3, false>);
   if (v2) {
     e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes - kSeqStaticLds);
     if (e != hipSuccess) return e;
@@ -1263,7 +1313,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   else if (!v2) hipLaunchKernelGGL(k_lstm_seq<false>, grid, block, lds, s, a);
   else if (!a.xpre) hipLaunchKernelGGL((k_lstm_seq2<false, 1, true>), grid, block, lds, s, a);
   else if (K == 1) hipLaunchKernelGGL((k_lstm_seq2<true, 1, true>), grid, block, lds, s, a);
-  else hipLaunchKernelGGL((k_lstm_seq2<true, 3, true>), grid, block, lds, s, a);
+  else hipLaunchKernelGGL((k_lstm_seq2<true, 3, false>), grid, block, lds, s, a);
   return hipGetLastError();
 }
 
