@@ -846,16 +846,16 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
           w[2 * s + 1] = wq[s * 128 + 32];
         }
       };
-      TileOps tob[PF ? 2 : 1];
-      load_tile(0, tob[0]);
-      // PF: unrolled, the next tile's loads in flight; else a real loop (one
-      // tile's registers live at a time)
-#pragma unroll(PF ? kRT : 1)
+      // a real loop over the tiles (unrolled, the scheduler mixes the tiles'
+      // registers and spills); PF: the next tile's loads are issued into a
+      // second register set before this tile's MFMAs, and moved over after
+      TileOps to, tn;
+      load_tile(0, to);
+#pragma unroll 1
       for (int rt = 0; rt < kRT; ++rt) {
-        TileOps& to = tob[PF ? (rt & 1) : 0];
         float4 (&tk)[4][KK] = to.tk;
-        if (PF && rt + 1 < kRT) load_tile(rt + 1, tob[PF ? ((rt + 1) & 1) : 0]);  // in flight now
-        else if (!PF && rt > 0) load_tile(rt, tob[0]);
+        if (PF && rt + 1 < kRT) load_tile(rt + 1, tn);  // in flight now
+        else if (!PF && rt > 0) load_tile(rt, to);
         f32x16 acc[2];
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct)
@@ -896,7 +896,10 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
         }
         // gate update of this tile: lane (row, hh) of tile ct holds gates g = 0..3
         // of units 16u + 8ct + 4hh + m in acc[ct][4g + m]
-        if (row_n(rt) >= M) continue;
+        if (row_n(rt) >= M) {
+          if (PF) to = tn;
+          continue;
+        }
         const int64_t rr = (int64_t(t) * N + n) * M + row_n(rt);
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
@@ -955,6 +958,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
               *reinterpret_cast<float4*>(ap + 4 * m) = make_float4(zz[m], ii[m], ff[m], oo[m]);
           }
         }
+        if (PF) to = tn;
       }
       if (stamp) CG_TS(A.ts, 3);
       // the next step's phase 1 reloads h into slot0, which holds this step's
