@@ -65,6 +65,7 @@ struct GrpFwdArgs {
   int64_t plane;    // N*M*Fin
   float* yp;        // [G][N*M][Fout] partial y per group, or NULL (basis only)
   unsigned long long* ts;  // ablation build: phase stamps (CG_TS), else NULL
+  int dbg;                 // ablation build (k_grp16_fwd): 1 no MFMA, 2 no SpMM, 4 no plane stores
 };
 
 template <int NOT>  // 32-wide output tiles (Fout <= 32 * NOT)
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
       for (int e = 0; e < 16; ++e) acc[rt][ot][e] = 0.f;
   __syncthreads();
   for (int k = 0; k < K; ++k) {
-    if (want_y) {
+    if (want_y && !CG_DBG(A.dbg, 1)) {
       // y^T[out][row] += W_k^T[out][ch] T_k^T[ch][row], channels 8hh + s
       const float* wk = s_W + k * 512 * NOT + hh * 32 * NOT + j;
       float4 ta[kGRT], tb[kGRT];
@@ -304,6 +305,10 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
         for (int hf = 0; hf < 2; ++hf) {
           if (!rvS[rt][hf]) continue;
           float4 sm;
+          if (CG_DBG(A.dbg, 2)) {  // ablation: no gathers
+            nv[rt][hf] = tm1[rt][hf];
+            continue;
+          }
           const int b0 = rbl[rt][hf] & 0xffff, b1 = b0 + (rbl[rt][hf] >> 16);
           with_row_len(wl[rt][hf], [&](auto lc) {
             sm = lds_row_spmm<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
@@ -324,7 +329,8 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
           float4* own = reinterpret_cast<float4*>(slot + rowS[rt][hf] * kGQ16 + 4 * qs);
           tm1[rt][hf] = *own;
           *own = nv[rt][hf];
-          *reinterpret_cast<float4*>(pl + (int64_t(n) * M + rowS[rt][hf]) * Fin + c0) = nv[rt][hf];
+          if (!CG_DBG(A.dbg, 4))
+            *reinterpret_cast<float4*>(pl + (int64_t(n) * M + rowS[rt][hf]) * Fin + c0) = nv[rt][hf];
         }
       __syncthreads();
     }
@@ -802,6 +808,7 @@ hipError_t launch_grp_fwd(const int* rowptr, const int* col, const float* val, c
                int64_t(N) * M * Fin, y ? yp : nullptr, nullptr};
 #ifdef CG_DEBUG
   a.ts = g_debug_ts;
+  a.dbg = (debug_flags() >> 24) & 0xff;
 #endif
   const size_t lds = g16 ? grp16_fwd_lds(M, K, Fout, nnz) : grp_fwd_lds(M, K, Fout, nnz);
   if (g16 && Fout <= 32) {
