@@ -43,6 +43,12 @@ constexpr int kGQ = 8;    // channels per group
 constexpr int kGRT = 4;   // 32-row tiles per wave (8 waves x 4 x 32 = 1024 rows)
 constexpr int kGQ16 = 16; // channels per group of the one-slot kernels (Fin % 16 == 0)
 
+// CG_SPMM_PW=0: the resident SpMMs read their CSR metadata one entry per LDS
+// access (lds_row_spmm) instead of two (lds_row_spmm_w); A/B runs, read per call
+inline bool spmm_pw() {
+  const char* e = getenv("CG_SPMM_PW");
+  return !(e && e[0] == '0');
+}
 inline int rup(int v, int m) { return (v + m - 1) / m * m; }
 
 // block -> (sample, group): the G groups of a sample on one XCD
@@ -208,8 +214,9 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
 // T_{k-1} of its own rows in registers, a barrier, the lane swaps its rows'
 // T_k out for T_{k+1}, a barrier.  SpMM lanes: (row lane / 4 of a 16-row half
 // tile, channels 4 (lane % 4) ..); MFMA lanes: (row j, channels 8hh .. 8hh+7).
-// Fout <= 32 only (NOT = 1; two output tiles spill at 256 registers).
-template <int NOT>
+// Fout <= 32 only (NOT = 1; two output tiles spill at 256 registers).  PW: the
+// rows' CSR metadata read two entries per LDS access (lds_row_spmm_w).
+template <int NOT, bool PW>
 __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -311,7 +318,10 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
           }
           const int b0 = rbl[rt][hf] & 0xffff, b1 = b0 + (rbl[rt][hf] >> 16);
           with_row_len(wl[rt][hf], [&](auto lc) {
-            sm = lds_row_spmm<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
+            if constexpr (PW)
+              sm = lds_row_spmm_w<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
+            else
+              sm = lds_row_spmm<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
           });
           if (k >= 1) {
             const float4 p = tm1[rt][hf];
@@ -812,10 +822,14 @@ hipError_t launch_grp_fwd(const int* rowptr, const int* col, const float* val, c
 #endif
   const size_t lds = g16 ? grp16_fwd_lds(M, K, Fout, nnz) : grp_fwd_lds(M, K, Fout, nnz);
   if (g16 && Fout <= 32) {
-    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp16_fwd<1>),
+    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp16_fwd<1, true>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    static hipError_t at0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp16_fwd<1, false>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
     if (at != hipSuccess) return at;
-    hipLaunchKernelGGL(k_grp16_fwd<1>, dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+    if (at0 != hipSuccess) return at0;
+    if (spmm_pw()) hipLaunchKernelGGL((k_grp16_fwd<1, true>), dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+    else hipLaunchKernelGGL((k_grp16_fwd<1, false>), dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
   } else if (Fout <= 32) {
     static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_fwd<1>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);

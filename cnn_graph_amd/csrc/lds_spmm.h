@@ -55,6 +55,66 @@ __device__ __forceinline__ float4 lds_row_spmm(const float* X, int stride, int c
   return s;
 }
 
+// lds_row_spmm with the row's CSR metadata read two entries per LDS access:
+// the 16-bit columns as 32-bit words and the values as 64-bit pairs from the
+// even-aligned entry at or below rb, so a row of L entries takes
+// 2 ceil((L + 1) / 2) metadata reads + L gathers instead of 3L LDS accesses.
+// Entry e sits at word / pair (e + a) >> 1, half (e + a) & 1, a = rb & 1 (per
+// lane: a select); entries past the row end gather the zero row with value 0,
+// exactly as lds_row_spmm (the words read past the CSR's end feed only those).
+// col must be 4-byte and val 8-byte aligned; the sum is lds_row_spmm's.
+template <int L>
+__device__ __forceinline__ float4 lds_row_spmm_w(const float* X, int stride, int c0,
+                                                 const unsigned short* col, const float* val,
+                                                 int rb, int re, int zrow) {
+#pragma clang fp contract(off)
+  if constexpr (L == 0) {
+    return lds_row_spmm<0>(X, stride, c0, col, val, rb, re, zrow);
+  } else {
+    constexpr int NW = (L + 2) / 2;  // words / pairs covering entries 0 .. L-1 at either parity
+    const int a = rb & 1, r0 = rb - a;
+    unsigned cw[NW];
+    float2 vw[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      cw[i] = *reinterpret_cast<const unsigned*>(col + r0 + 2 * i);
+      vw[i] = *reinterpret_cast<const float2*>(val + r0 + 2 * i);
+    }
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int c[L];
+    float w[L];
+#pragma unroll
+    for (int e = 0; e < L; ++e) {
+      const bool ok = rb + e < re;
+      // entry e: word (e + a) >> 1, half (e + a) & 1
+      const unsigned wlo = cw[e >> 1], whi = cw[(e + 1) >> 1];
+      const float2 plo = vw[e >> 1], phi = vw[(e + 1) >> 1];
+      unsigned cword;
+      float v;
+      if (e & 1) {  // (e + a) >> 1 = e/2 + a: the word changes with a, the half is 1 - a
+        cword = a ? (whi & 0xffffu) : (wlo >> 16);
+        v = a ? phi.x : plo.y;
+      } else {      // (e + a) >> 1 = e/2: the same word, half a
+        cword = a ? (wlo >> 16) : (wlo & 0xffffu);
+        v = a ? plo.y : plo.x;
+      }
+      c[e] = ok ? int(cword) : zrow;
+      w[e] = ok ? v : 0.f;
+    }
+    float4 g[L];
+#pragma unroll
+    for (int e = 0; e < L; ++e) g[e] = *reinterpret_cast<const float4*>(X + c[e] * stride + c0);
+#pragma unroll
+    for (int e = 0; e < L; ++e) {
+      s.x = s.x + w[e] * g[e].x;
+      s.y = s.y + w[e] * g[e].y;
+      s.z = s.z + w[e] * g[e].z;
+      s.w = s.w + w[e] * g[e].w;
+    }
+    return s;
+  }
+}
+
 // The same product with the row's columns already in registers: pk holds the
 // row's (up to 2*NP) column indices packed two per word (entry e in bits
 // 16*(e & 1) of pk[e / 2]; entries past the row hold zrow).  The gathers no

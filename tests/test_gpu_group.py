@@ -160,3 +160,30 @@ def test_group_side_stream_dw_bitwise(dev, monkeypatch, layout):
     for (dx0, dW0), (dx1, dW1) in zip(out["0"], out["1"]):
         assert torch.equal(dx0, dx1)
         assert torch.equal(dW0, dW1)
+
+
+@pytest.mark.parametrize("gname,N,Fin,K,Fout", [("golden_E.npz", 3, 32, 20, 32), ("golden_B.npz", 2, 16, 5, 32),
+                                                ("golden_B.npz", 2, 32, 7, 20)])
+def test_group_fwd_paired_metadata_bitwise(dev, monkeypatch, gname, N, Fin, K, Fout):
+    """k_grp16_fwd with the CSR metadata read two entries per LDS access
+    (lds_row_spmm_w, default) against one per access (CG_SPMM_PW=0): basis
+    planes and y bitwise equal (rows start at both parities of the CSR)."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden(gname))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    assert (np.asarray(c["Lt_rowptr"][:-1]) % 2 == 1).any()
+    rng = np.random.default_rng(N + Fin + K + Fout + 11)
+    xt = _t(rng.standard_normal((N, M, Fin)), dev)
+    Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
+    out = {}
+    for pw in ("1", "0"):
+        monkeypatch.setenv("CG_SPMM_PW", pw)
+        plan = ChebPlan(Lt, device=0, path="stream")
+        r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="planes")
+        r.forward(xt, Wt)
+        torch.cuda.synchronize()
+        out[pw] = (r.basis.clone(), r.y.clone())
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert torch.equal(out["1"][1], out["0"][1])
