@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
         if (!rvS[rt]) continue;
         float4 sm;
         with_row_len(wl[rt], [&](auto lc) {
-          sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hs, s_col, s_val, rb[rt], re[rt], M);
+          sm = lds_row_spmm_w<decltype(lc)::value>(cur, kGQ, 4 * hs, s_col, s_val, rb[rt], re[rt], M);
         });
         float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
         float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kGQ + 4 * hs);
@@ -493,11 +493,11 @@ __global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
             if constexpr (LL > 0 && LL <= 2 * NP)
               sm = lds_row_spmm_pc<LL, NP, 3>(cur, 4 * hh, pk[rt], s_val, rb[rt], re[rt]);
             else
-              sm = lds_row_spmm<LL>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+              sm = lds_row_spmm_w<LL>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
           });
         } else {
           with_row_len(wl[rt], [&](auto lc) {
-            sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+            sm = lds_row_spmm_w<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
           });
         }
       }
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
           float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
           if (rv[rt])
             with_row_len(wl[rt], [&](auto lc) {
-              sm = lds_row_spmm<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
+              sm = lds_row_spmm_w<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
             });
           const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
           float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kGQ + 4 * hh);

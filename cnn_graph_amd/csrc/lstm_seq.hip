@@ -378,7 +378,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
               }
               float4 sm;
               with_row_len(wl[rt], [&](auto lc) {
-                sm = lds_row_spmm<decltype(lc)::value>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
+                sm = lds_row_spmm_w<decltype(lc)::value>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
               });
               float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2);
               if (k >= 1) {
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
                 if (!rvS[rt] || CG_DBG(A.dbg, 2)) continue;
                 float4 sm;
                 with_row_len(wl[rt], [&](auto lc) {
-                  sm = lds_row_spmm<decltype(lc)::value>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
+                  sm = lds_row_spmm_w<decltype(lc)::value>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
                 });
                 float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
                 float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2);
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
                 if constexpr (LL > 0 && LL <= 2 * NP)
                   sm = lds_row_spmm_pc<LL, NP, 3>(cur, 4 * hs2, pk[rt], s_val, rb[rt], re[rt]);
                 else
-                  sm = lds_row_spmm<LL>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
+                  sm = lds_row_spmm_w<LL>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
               });
               float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
               float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2);
@@ -1162,7 +1162,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
       float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
       if (rows[rt] < M)
         with_row_len(wl[rt], [&](auto lc) {
-          sm = lds_row_spmm<decltype(lc)::value>(slot, kBS, 4 * q, s_col, s_val, rb[rt], re[rt], M);
+          sm = lds_row_spmm_w<decltype(lc)::value>(slot, kBS, 4 * q, s_col, s_val, rb[rt], re[rt], M);
         });
       const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
 #pragma unroll
