@@ -307,7 +307,36 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
     if (k + 1 < K) {
       float4 nv[kGRT][2];
 #pragma unroll
-      for (int rt = 0; rt < kGRT; ++rt)
+      for (int rt = 0; rt < kGRT; ++rt) {
+        if constexpr (PW) {
+          // both halves of the tile under ONE length switch (their rows are
+          // neighbours in the longest-first order, so the lengths nearly
+          // agree; a padding row has length 0 and sums to 0): the two rows'
+          // reads interleave in one basic block
+          float4 sm[2];
+          if (CG_DBG(A.dbg, 2)) {  // ablation: no gathers
+            sm[0] = tm1[rt][0];
+            sm[1] = tm1[rt][1];
+          } else {
+            const int a0 = rbl[rt][0] & 0xffff, a1 = a0 + (rbl[rt][0] >> 16);
+            const int b0 = rbl[rt][1] & 0xffff, b1 = b0 + (rbl[rt][1] >> 16);
+            with_row_len(wl[rt][0] > wl[rt][1] ? wl[rt][0] : wl[rt][1], [&](auto lc) {
+              constexpr int LL = decltype(lc)::value;
+              sm[0] = lds_row_spmm_w<LL>(slot, kGQ16, 4 * qs, s_col, s_val, a0, a1, M);
+              sm[1] = lds_row_spmm_w<LL>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
+            });
+          }
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            float4 v = sm[hf];
+            if (k >= 1 && !CG_DBG(A.dbg, 2)) {
+              const float4 p = tm1[rt][hf];
+              v = make_float4(2.f * v.x - p.x, 2.f * v.y - p.y, 2.f * v.z - p.z, 2.f * v.w - p.w);
+            }
+            nv[rt][hf] = v;
+          }
+          continue;
+        }
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           if (!rvS[rt][hf]) continue;
@@ -318,10 +347,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
           }
           const int b0 = rbl[rt][hf] & 0xffff, b1 = b0 + (rbl[rt][hf] >> 16);
           with_row_len(wl[rt][hf], [&](auto lc) {
-            if constexpr (PW)
-              sm = lds_row_spmm_w<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
-            else
-              sm = lds_row_spmm<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
+            sm = lds_row_spmm<decltype(lc)::value>(slot, kGQ16, 4 * qs, s_col, s_val, b0, b1, M);
           });
           if (k >= 1) {
             const float4 p = tm1[rt][hf];
@@ -329,6 +355,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
           }
           nv[rt][hf] = sm;
         }
+      }
       __syncthreads();  // every gather and contraction read of T_k done
       float* pl = A.basis + int64_t(k + 1) * A.plane;
 #pragma unroll
