@@ -731,13 +731,20 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
         const float* cur = ((K - 2 - k) & 1) ? slotB : slotA;
         float* nxt = ((K - 2 - k) & 1) ? slotA : slotB;
         const float c = k >= 1 ? 2.f : 1.f;
+        // tiles in pairs under ONE length switch (the longer row's bound; a
+        // padding row has rb = re = 0 and sums to 0): the two rows' reads
+        // interleave in one basic block
+        float4 smp[kGRT];
+#pragma unroll
+        for (int rp = 0; rp < kGRT; rp += 2)
+          with_row_len(wl[rp] > wl[rp + 1] ? wl[rp] : wl[rp + 1], [&](auto lc) {
+            constexpr int LL = decltype(lc)::value;
+            smp[rp] = lds_row_spmm_w<LL>(cur, kGQ, 4 * hh, s_col, s_val, rb[rp], re[rp], M);
+            smp[rp + 1] = lds_row_spmm_w<LL>(cur, kGQ, 4 * hh, s_col, s_val, rb[rp + 1], re[rp + 1], M);
+          });
 #pragma unroll
         for (int rt = 0; rt < kGRT; ++rt) {
-          float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (rv[rt])
-            with_row_len(wl[rt], [&](auto lc) {
-              sm = lds_row_spmm_w<decltype(lc)::value>(cur, kGQ, 4 * hh, s_col, s_val, rb[rt], re[rt], M);
-            });
+          const float4 sm = smp[rt];
           const float sv[4] = {sm.x, sm.y, sm.z, sm.w};
           float4* own = reinterpret_cast<float4*>(nxt + row[rt] * kGQ + 4 * hh);
           float g2[4] = {0.f, 0.f, 0.f, 0.f};
