@@ -802,13 +802,13 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
 size_t grp_fwd_lds(int M, int K, int Fout, int64_t nnz) {
   const int NOT = Fout <= 32 ? 1 : 2;
   return size_t(2) * rup(M + 1, 32) * kGQ * 4 + size_t(K) * 256 * NOT * 4 + size_t(nnz) * 4 +
-         align16(size_t(nnz) * 2);
+         align16(size_t(nnz) * 2 + kSpmmSlack);
 }
 
 size_t grp16_fwd_lds(int M, int K, int Fout, int64_t nnz) {
   const int NOT = Fout <= 32 ? 1 : 2;
   return size_t(rup(M + 1, 32)) * kGQ16 * 4 + size_t(K) * 512 * NOT * 4 + size_t(nnz) * 4 +
-         align16(size_t(nnz) * 2);
+         align16(size_t(nnz) * 2 + kSpmmSlack);
 }
 
 // the 16-channel forward serves Fin % 16 == 0, Fout <= 32 when its LDS fits
@@ -824,7 +824,7 @@ static bool grp16_enabled() {
 }
 
 size_t grp_clen_lds(int M, int64_t nnzT) {
-  return size_t(2) * rup(M + 1, 32) * kGQ * 4 + size_t(nnzT) * 4 + align16(size_t(nnzT) * 2);
+  return size_t(2) * rup(M + 1, 32) * kGQ * 4 + size_t(nnzT) * 4 + align16(size_t(nnzT) * 2 + kSpmmSlack);
 }
 
 bool grp_ok(int M, int64_t nnz, int Fin, int K, int Fout) {

@@ -55,6 +55,11 @@ __device__ __forceinline__ float4 lds_row_spmm(const float* X, int stride, int c
   return s;
 }
 
+// bytes of LDS kept past the end of the 16-bit column array by a kernel using
+// lds_row_spmm_w: a padded row at the CSR's end reads up to L + 1 - len <= 13
+// columns past it (and its values read on into the column array)
+constexpr int kSpmmSlack = 32;
+
 // lds_row_spmm with the row's CSR metadata read two entries per LDS access:
 // the 16-bit columns as 32-bit words and the values as 64-bit pairs from the
 // even-aligned entry at or below rb, so a row of L entries takes
@@ -62,7 +67,9 @@ __device__ __forceinline__ float4 lds_row_spmm(const float* X, int stride, int c
 // Entry e sits at word / pair (e + a) >> 1, half (e + a) & 1, a = rb & 1 (per
 // lane: a select); entries past the row end gather the zero row with value 0,
 // exactly as lds_row_spmm (the words read past the CSR's end feed only those).
-// col must be 4-byte and val 8-byte aligned; the sum is lds_row_spmm's.
+// col must be 4-byte and val 8-byte aligned; the sum is lds_row_spmm's.  A
+// kernel using it keeps kSpmmSlack bytes of LDS past its column array.
+
 template <int L>
 __device__ __forceinline__ float4 lds_row_spmm_w(const float* X, int stride, int c0,
                                                  const unsigned short* col, const float* val,

@@ -1214,7 +1214,7 @@ inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
 size_t lstm_seq_lds(int M, int K, int64_t nnz, int xfin) {
   return size_t(2) * round_up(M + 1, 32) * kQ * 4 + size_t(K) * 2048 * 4 +
          (xfin > 0 ? size_t(K) * 512 * 4 : 0) + 512 + size_t(nnz) * 4 +
-         align16(size_t(nnz) * 2);
+         align16(size_t(nnz) * 2 + kSpmmSlack);
 }
 
 bool lstm_seq_ok(int M, int H, int K, int64_t nnz, int xfin) {
@@ -1224,7 +1224,7 @@ bool lstm_seq_ok(int M, int H, int K, int64_t nnz, int xfin) {
 
 size_t lstm_bstep_lds(int M, int K, int64_t nnzT) {
   return size_t(round_up(M + 1, 16)) * kBS * 4 + size_t(K) * 2048 * 4 + size_t(nnzT) * 4 +
-         align16(size_t(nnzT) * 2);
+         align16(size_t(nnzT) * 2 + kSpmmSlack);
 }
 
 bool lstm_bstep_ok(int M, int H, int K, int64_t nnzT) {
