@@ -426,20 +426,16 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
             if (k + 1 < K) {
               // T_{k+1} of this lane's rows / channels: CSR order from +0
               float* nxt = (k & 1) ? slot0 : slot1;
-              // tiles in pairs under ONE length switch (a padding row has
-              // rb = re = 0 and sums to 0): the two rows' reads interleave
-              float4 smp[kRT];
-#pragma unroll
-              for (int rp = 0; rp < kRT; rp += 2)
-                with_row_len(wl[rp] > wl[rp + 1] ? wl[rp] : wl[rp + 1], [&](auto lc) {
-                  constexpr int LL = decltype(lc)::value;
-                  smp[rp] = lds_row_spmm_w<LL>(cur, kQ, 4 * hs2, s_col, s_val, rb[rp], re[rp], M);
-                  smp[rp + 1] = lds_row_spmm_w<LL>(cur, kQ, 4 * hs2, s_col, s_val, rb[rp + 1], re[rp + 1], M);
-                });
 #pragma unroll
               for (int rt = 0; rt < kRT; ++rt) {
                 if (!rvS[rt] || CG_DBG(A.dbg, 2)) continue;
-                const float4 sm = smp[rt];
+                // one row per length switch here: the paired form (as in the
+                // BPTT step) measured 1-1.5 % slower on config E (profiles/r04_final2)
+                float4 sm;
+                with_row_len(wl[rt], [&](auto lc) {
+                  sm = lds_row_spmm_w<decltype(lc)::value>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
+                });
+
                 float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
                 float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2);
                 if (k >= 1) {  // T_{k-1} of this row: the slot being overwritten
