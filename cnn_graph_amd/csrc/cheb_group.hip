@@ -585,6 +585,7 @@ struct GrpClenDyArgs {
   int dx_acc;
   int pipe;  // 1: the next group's tiles during this group's steps; 0: each group's up front
   unsigned long long* ts;  // ablation build: phase stamps (CG_TS), else NULL
+  int dbg;  // ablation build: 1 no D-tile MFMAs, 2 no SpMM, 4 no dy loads, 8 no hand-over
 };
 
 template <int KC2>  // Fout / 2: the row GEMM's inner half (16 or 32)
@@ -637,6 +638,11 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
   // dy operand of tile rt (the MFMA lane's half row: KC2 floats), loaded ahead
   // of its MFMAs (global / L2: the sample's dy is read by every group)
   auto dload = [&](int rt, float (&b)[KC2]) {
+    if (CG_DBG(A.dbg, 4)) {  // ablation: no dy loads
+#pragma unroll
+      for (int q = 0; q < KC2; ++q) b[q] = float(q);
+      return;
+    }
     const float* dr = A.dy + (int64_t(n) * M + (drow[rt] >= 0 ? drow[rt] : 0)) * Fout + mh * KC2;
     if constexpr (KC2 % 4 == 0) {
 #pragma unroll
@@ -656,6 +662,10 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
     const float* wr = s_w + ((kk < K ? kk : 0) * kGQ + (mi & 7)) * WS + mh * KC2;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    if (CG_DBG(A.dbg, 1)) {  // ablation: no D-tile MFMAs
+      acc[0] = b[0];
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < KC2; ++q) {
       const float a = kk < K ? wr[q] : 0.f;
@@ -675,7 +685,9 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
     for (int ko = 0; ko < 4; ++ko)
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const float v = __int_as_float(__builtin_amdgcn_ds_bpermute(bsrc, __float_as_int(acc[4 * ko + m])));
+        const float v = CG_DBG(A.dbg, 8)  // ablation: no hand-over
+                            ? acc[4 * ko + m]
+                            : __int_as_float(__builtin_amdgcn_ds_bpermute(bsrc, __float_as_int(acc[4 * ko + m])));
         if (odd) Dg[ko][rt][m] = v;
         else Dg[rt][ko][m] = v;
       }
@@ -737,6 +749,9 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
         float4 smp[kGRT];
 #pragma unroll
         for (int rp = 0; rp < kGRT; rp += 2)
+          if (CG_DBG(A.dbg, 2)) {  // ablation: no SpMM
+            smp[rp] = smp[rp + 1] = make_float4(1.f, 1.f, 1.f, 1.f);
+          } else
           with_row_len(wl[rp] > wl[rp + 1] ? wl[rp] : wl[rp + 1], [&](auto lc) {
             constexpr int LL = decltype(lc)::value;
             smp[rp] = lds_row_spmm_w<LL>(cur, kGQ, 4 * hh, s_col, s_val, rb[rp], re[rp], M);
@@ -940,6 +955,7 @@ hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* 
                   Fout / 2, dy, W, dx, dx_acc, pipe, nullptr};
 #ifdef CG_DEBUG
   a.ts = g_debug_ts;
+  a.dbg = (debug_flags() >> 24) & 0xff;
 #endif
   static hipError_t at16 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen_dy<16>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);

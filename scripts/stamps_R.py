@@ -6,8 +6,10 @@ k_grp_clen_dy (0 start, 1 prologue done, 2..6 order groups done, 7 dx stored).
 Per kernel: median us of each stamp from the workgroup's own start, and the
 distribution of workgroup start times (residency rounds), plus the HIP-event
 time of 20 calls.  An optional argument sets k_grp16_fwd's ablation flags
-(debug byte 24-31: 1 no MFMA, 2 no SpMM, 4 no plane stores; outputs garbage,
-times only) for the forward.   python3 scripts/stamps_R.py [FLAGS]"""
+(debug byte 24-31; k_grp16_fwd: 1 no MFMA, 2 no SpMM, 4 no plane stores;
+k_grp_clen_dy: 1 no D-tile MFMAs, 2 no SpMM, 4 no dy loads, 8 no hand-over;
+outputs garbage, times only) for the named call.
+  python3 scripts/stamps_R.py [FLAGS [fwd|bwd]]"""
 import ctypes
 import json
 import os
@@ -59,13 +61,14 @@ def main():
     h.cg_debug_set_ts.argtypes = [ctypes.c_void_p]
     out = {}
     flags = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    which = sys.argv[2] if len(sys.argv) > 2 else "fwd"  # the call the flags apply to
     h.cg_debug_set_flags.argtypes = [ctypes.c_int]
     if flags:
         h.cg_debug_set_flags(flags << 24)
         out["flags"] = flags
     for name, fn in (("fwd", lambda: r.forward(x, W)), ("bwd", lambda: r.backward(dy, W))):
-        if flags and name == "bwd":
-            break
+        if flags and name != which:
+            continue
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
