@@ -1,6 +1,6 @@
 #!/bin/bash
-# r04: config R with k_grp_clen_dy's opposite phase order per SIMD (k_grp16_fwd)
-# (scripts/dbg/libcheb_alt_o.so) vs pairs (default library), alternating.
+# r04: config R with k_grp16_fwd's two waves per SIMD in opposite MFMA / SpMM phase order
+# (scripts/dbg/libcheb_alt_o.so) vs one order (default library), alternating.
 #   bash scripts/gpu_r04_alto.sh TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
