@@ -25,6 +25,9 @@ VARIANTS = {"auto": CG_VARIANT_AUTO, "classic": CG_VARIANT_CLASSIC,
             "steps": CG_VARIANT_STEPS}
 CG_BASIS_ROWS, CG_BASIS_ORDERS, CG_BASIS_PLANES = 0, 1, 2
 BASIS_LAYOUTS = {"rows": CG_BASIS_ROWS, "orders": CG_BASIS_ORDERS, "planes": CG_BASIS_PLANES}
+# kernel-selection options (cg_set_option; include/cheb_mi355.h CG_OPT_*)
+OPTIONS = {"dw_direct": 0, "dw_w2": 1, "dw_waves": 2, "spmm_pw": 3, "grp16": 4, "grp_pc": 5,
+           "clen_dy": 6, "seq_xpre": 7}
 
 
 class CGError(RuntimeError):
@@ -114,6 +117,9 @@ _SIGNATURES = {
                              _vp, _vp, _vp, _vp, _c_i64, _vp, _c_sz, _vp], _c_int),
     "cg_lstm_seq_status": ([_vp, _c_i32, _vp, ctypes.POINTER(_c_i32), _vp], _c_int),
     "cg_lstm_seq_fault": ([_vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32)], _c_int),
+    "cg_plan_set_seq_fault_test": ([_vp, _c_i32], _c_int),
+    "cg_set_option": ([_c_i32, _c_i32], _c_int),
+    "cg_get_option": ([_c_i32, ctypes.POINTER(_c_i32)], _c_int),
     "cg_dropout_forward": ([_vp, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, _vp, _vp], _c_int),
     "cg_dropout_backward": ([_vp, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, _vp, _vp], _c_int),
     "cg_clip_by_norm": ([_vp, ctypes.c_int64, ctypes.c_float, _vp, _vp], _c_int),
@@ -178,6 +184,36 @@ def check(func_name: str, status: int):
     if status != CG_OK:
         msg = lib().cg_last_error()
         raise CGError(func_name, status, msg.decode() if msg else "")
+
+
+def get_option(name: str) -> int:
+    v = ctypes.c_int32()
+    call("cg_get_option", OPTIONS[name], ctypes.byref(v))
+    return v.value
+
+
+def set_option(name: str, value: int) -> int:
+    """Set a kernel-selection option (process-wide); returns the previous value."""
+    old = get_option(name)
+    call("cg_set_option", OPTIONS[name], int(value))
+    return old
+
+
+class options:
+    """Context manager: ``with _lib.options(dw_direct=0): ...`` restores on exit."""
+
+    def __init__(self, **kw):
+        self.kw, self.saved = kw, {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.saved[k] = set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            set_option(k, v)
+        return False
 
 
 def call(func_name: str, *args):

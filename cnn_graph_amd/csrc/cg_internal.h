@@ -21,6 +21,12 @@ constexpr int kLdsBytes = 160 * 1024;  // gfx950 LDS per CU
 __host__ __device__ inline int lds_vertex_stride(int M) { return ((M + 31) / 32) * 32 + 1; }
 __host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
+// Kernel-selection options (cg_set_option, CG_OPT_* in include/cheb_mi355.h):
+// process-wide, read by the launch code at every launch
+enum Opt { kOptDwDirect = 0, kOptDwW2, kOptDwWaves, kOptSpmmPw, kOptGrp16, kOptGrpPc, kOptClenDy,
+           kOptSeqXpre, kOptCount };
+int option(Opt o);
+
 // Timing-ablation switches (bits 0-7 forward resident kernel, 8-15 backward,
 // 22 skip dW, 23 skip the slab reduction; outputs are WRONG when set).  They
 // exist only in the ablation build (`make debug`, -DCG_DEBUG, a separate .so

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -66,11 +67,10 @@ struct cg_plan {
   int* seq_fault_dev = nullptr;  // its device alias
   hipEvent_t seq_event = nullptr;
   bool seq_launched = false;
-  // side stream of the backward: dW (basis^T dy) runs on it concurrently with
-  // the dx recurrence, which does not read dW (fork / join by events, so it
-  // also works under stream capture); created on first use
-  hipStream_t side = nullptr;
-  hipEvent_t side_fork = nullptr, side_join = nullptr;
+  // test hook (cg_plan_set_seq_fault_test): >= 0 makes workgroup 0 of pair 0
+  // of this plan's sequence launches stop publishing its step counter from
+  // that step on; -1 (default) off
+  int seq_fault_test = -1;
 };
 
 namespace {
@@ -290,29 +290,7 @@ void free_plan(cg_plan* p) {
   if (p->tfast.buf) (void)hipFree(p->tfast.buf);
   if (p->seq_event) (void)hipEventDestroy(p->seq_event);
   if (p->seq_fault) (void)hipHostFree(p->seq_fault);
-  if (p->side_fork) (void)hipEventDestroy(p->side_fork);
-  if (p->side_join) (void)hipEventDestroy(p->side_join);
-  if (p->side) (void)hipStreamDestroy(p->side);
   delete p;
-}
-
-// CG_SIDE_DW=1: dW on the plan's side stream, concurrent with the channel-group
-// recurrence k_grp_clen_dy (whose 400 workgroups of one per CU run in two
-// rounds on config R, the second 56 % full).  Off by default: measured 5.32
-// vs 4.90-4.92 ms per R step (profiles/r04_f) -- the dW workgroups take CUs as
-// the first round drains and the recurrence's second round starts up to 240
-// instead of 117 us into the call (phase stamps).  Read per call.
-int side_dw_mode() {
-  const char* e = getenv("CG_SIDE_DW");
-  return (e && e[0]) ? atoi(e) : 0;
-}
-
-int side_ready(cg_plan* p) {
-  if (p->side) return CG_OK;
-  CG_HIP(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
-  CG_HIP(hipEventCreateWithFlags(&p->side_fork, hipEventDisableTiming));
-  CG_HIP(hipEventCreateWithFlags(&p->side_join, hipEventDisableTiming));
-  return CG_OK;
 }
 
 int check_device(const cg_plan* p) {
@@ -476,9 +454,41 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
 
 }  // namespace
 
+namespace cg {
+namespace {
+// CG_OPT_* values (defaults: the measured-faster kernels) and their ranges
+std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}};
+bool option_valid(int o, int v) {
+  switch (o) {
+    case kOptDwDirect: return v >= 0 && v <= 3;
+    case kOptDwWaves: return v == 4 || v == 8;
+    case kOptClenDy: return v >= 0 && v <= 2;
+    default: return v == 0 || v == 1;
+  }
+}
+}  // namespace
+int option(Opt o) { return g_opts[o].load(std::memory_order_relaxed); }
+}  // namespace cg
+
 extern "C" {
 
 int cg_version(void) { return 201; }
+
+
+int cg_set_option(int32_t option, int32_t value) {
+  if (option < 0 || option >= cg::kOptCount) return fail(CG_ERR_ARG, "unknown option %d", option);
+  if (!cg::option_valid(option, value))
+    return fail(CG_ERR_ARG, "value %d out of range for option %d", value, option);
+  cg::g_opts[option].store(value, std::memory_order_relaxed);
+  return ok();
+}
+
+int cg_get_option(int32_t option, int32_t* value) {
+  if (option < 0 || option >= cg::kOptCount || !value)
+    return fail(CG_ERR_ARG, "unknown option %d or null value", option);
+  *value = cg::g_opts[option].load(std::memory_order_relaxed);
+  return ok();
+}
 
 #ifdef CG_DEBUG
 // Timing-ablation hook of the debug build only (`make debug`; not in the
@@ -881,8 +891,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   const int64_t R = int64_t(N) * M;
   const int chunks = cg::dw_chunks(R);
 
-  // Everything runs on the caller's stream except the channel-group path's dW
-  // (side_dw_mode).  (Forking the streaming dW GEMM onto a side stream to
+  // Everything runs on the caller's stream.  (Forking the streaming dW GEMM onto a side stream to
   // overlap the dx recurrence was measured on MI355X in round 1: the event
   // fork + join costs ~20 us per call, more than the overlap gains there.)
   char* base = static_cast<char*>(workspace);
@@ -893,7 +902,6 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   const bool fused =
       dx != nullptr && dW != nullptr && path == CG_PATH_RESIDENT && fused_dw(plan, Fin, K, Fout);
   int nslab_ready = 0;  // dW slabs a kernel of the dx pass already wrote
-  bool dw_done = false;  // dW slabs launched on the side stream
   auto launch_dw = [&](hipStream_t st) -> hipError_t {
     if (cg::debug_flags() & (1 << 22)) return hipSuccess;  // ablation hook (debug build): skip dW
     return cg::launch_dw_slabs(basis, dy, R, FinK, Fout, slabs, st,
@@ -962,23 +970,9 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
     } else if (!stream_ws(plan, N, Fin, K, Fout).wide && use_group(plan, Fin, K, Fout) &&
                cg::grp_clen_dy_ok(M, plan->nnzT, K, Fout)) {
       // the whole reverse recurrence in LDS per (sample, 8 channels), dBasis
-      // formed in the kernel from dy and W (no dBasis planes); dW on the side
-      // stream with CG_SIDE_DW=1 (side_dw_mode)
-      const bool side = dW && side_dw_mode() >= 1;
-      if (side) {
-        const int rc = side_ready(plan);
-        if (rc) return rc;
-        CG_HIP(hipEventRecord(plan->side_fork, s));
-      }
+      // formed in the kernel from dy and W (no dBasis planes)
       CG_HIP(cg::launch_grp_clen_dy(plan->trowptr, plan->tcol, plan->tval, plan->tlorder, plan->nnzT,
                                     N, M, Fin, K, Fout, dy, W, dx, dx_acc, s));
-      if (side) {
-        CG_HIP(hipStreamWaitEvent(plan->side, plan->side_fork, 0));
-        CG_HIP(launch_dw(plan->side));
-        CG_HIP(hipEventRecord(plan->side_join, plan->side));
-        CG_HIP(hipStreamWaitEvent(s, plan->side_join, 0));
-        dw_done = true;
-      }
     } else {
       float* dA = reinterpret_cast<float*>(rest);
       const int NM = N * M;
@@ -1032,7 +1026,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   }
   if (!dW) return ok();
   if (fused) nslab_ready = N;
-  if (!nslab_ready && !dw_done) CG_HIP(launch_dw(s));
+  if (!nslab_ready) CG_HIP(launch_dw(s));
   const int nslab = nslab_ready ? nslab_ready : chunks;
   if (adam)  // reduction + optimizer step in one launch (no exchange in between)
     CG_HIP(cg::launch_reduce_slabs_adam(slabs, nslab, int64_t(FinK) * Fout, dW, *adam, s));
@@ -1669,15 +1663,11 @@ static int lstm_seq_impl(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t
     plan->seq_fault_dev = static_cast<int*>(dp);
     CG_HIP(hipEventCreateWithFlags(&plan->seq_event, hipEventDisableTiming));
   }
-  // fault injection for the tests (a pair whose workgroup 0 stops publishing
-  // from step CG_SEQ_INJECT_HANG on): read at every launch
-  const char* inj = getenv("CG_SEQ_INJECT_HANG");
-  const int inject_t = (inj && inj[0]) ? atoi(inj) : -1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   CG_HIP(cg::launch_lstm_seq(gates, T, N, plan->M, K, plan->nnz, plan->rowptr, plan->col, plan->val,
                              plan->lorder, xs, Wx, Fin, xplanes, xplane_stride, gx, Wh, bias, h0,
                              c0, hs, cs, act, planes, plane_stride, flags, plan->seq_fault_dev, P, s,
-                             inject_t));
+                             plan->seq_fault_test));
   CG_HIP(hipEventRecord(plan->seq_event, s));
   plan->seq_launched = true;
   return ok();
@@ -1731,6 +1721,12 @@ int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, in
   (void)workspace;  // the fault word lives in the plan (sticky), not in the workspace
   CG_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
   return cg_lstm_seq_fault(const_cast<cg_plan*>(plan), 1, 0, status);
+}
+
+int cg_plan_set_seq_fault_test(cg_plan* plan, int32_t step) {
+  if (!plan || step < -1) return fail(CG_ERR_ARG, "plan_set_seq_fault_test: bad arguments");
+  plan->seq_fault_test = step;
+  return ok();
 }
 
 int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,

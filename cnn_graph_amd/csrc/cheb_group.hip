@@ -43,12 +43,9 @@ constexpr int kGQ = 8;    // channels per group
 constexpr int kGRT = 4;   // 32-row tiles per wave (8 waves x 4 x 32 = 1024 rows)
 constexpr int kGQ16 = 16; // channels per group of the one-slot kernels (Fin % 16 == 0)
 
-// CG_SPMM_PW=0: the resident SpMMs read their CSR metadata one entry per LDS
-// access (lds_row_spmm) instead of two (lds_row_spmm_w); A/B runs, read per call
-inline bool spmm_pw() {
-  const char* e = getenv("CG_SPMM_PW");
-  return !(e && e[0] == '0');
-}
+// CG_OPT_SPMM_PW = 0: the resident SpMMs read their CSR metadata one entry per
+// LDS access (lds_row_spmm) instead of two (lds_row_spmm_w); A/B runs
+inline bool spmm_pw() { return option(kOptSpmmPw) != 0; }
 inline int rup(int v, int m) { return (v + m - 1) / m * m; }
 
 // block -> (sample, group): the G groups of a sample on one XCD
@@ -827,16 +824,10 @@ size_t grp16_fwd_lds(int M, int K, int Fout, int64_t nnz) {
 }
 
 // the 16-channel forward serves Fin % 16 == 0, Fout <= 32 when its LDS fits
-// (CG_GRP16=0 in the environment keeps the 8-channel one, for A/B runs).  A
-// 16-channel one-slot Clenshaw kernel (dx bitwise the same) was measured
-// slower than the 8-channel one on config R (160 vs 148 us) and dropped.
-static bool grp16_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("CG_GRP16");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// (CG_OPT_GRP16 = 0 keeps the 8-channel one, for A/B runs).  A 16-channel
+// one-slot Clenshaw kernel (dx bitwise the same) was measured slower than the
+// 8-channel one on config R (160 vs 148 us) and dropped.
+static bool grp16_enabled() { return option(kOptGrp16) != 0; }
 
 size_t grp_clen_lds(int M, int64_t nnzT) {
   return size_t(2) * rup(M + 1, 32) * kGQ * 4 + size_t(nnzT) * 4 + align16(size_t(nnzT) * 2 + kSpmmSlack);
@@ -914,9 +905,8 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (at0 != hipSuccess) return at0;
   if (at1 != hipSuccess) return at1;
-  // CG_GRP_PC=0: columns read from LDS every step (A/B; dx bitwise the same)
-  const char* pc = getenv("CG_GRP_PC");
-  if (pc && pc[0] == '0')
+  // CG_OPT_GRP_PC = 0: columns read from LDS every step (A/B; dx bitwise the same)
+  if (option(kOptGrpPc) == 0)
     hipLaunchKernelGGL(k_grp_clen<false>, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
   else
     hipLaunchKernelGGL(k_grp_clen<true>, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
@@ -925,18 +915,14 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
 
 // the fused variant serves Fout 2, 32 and 64 (the row GEMM's inner split
 // KC2 = Fout / 2: 1, 16, 32 -- the ResGNN's output layer and hidden layers);
-// CG_CLEN_DY=0 in the environment keeps the row GEMM + k_grp_clen pair (A/B runs)
+// CG_OPT_CLEN_DY = 0 keeps the row GEMM + k_grp_clen pair (A/B runs)
 
 size_t grp_clen_dy_lds(int M, int64_t nnzT, int K, int Fout) {
   return grp_clen_lds(M, nnzT) + size_t(K) * kGQ * (Fout + 4) * 4;
 }
 
 bool grp_clen_dy_ok(int M, int64_t nnzT, int K, int Fout) {
-  static const bool on = [] {
-    const char* e = getenv("CG_CLEN_DY");
-    return !(e && e[0] == '0');
-  }();
-  return on && (Fout == 2 || Fout == 32 || Fout == 64) && M <= kGRT * 8 * 32 &&
+  return option(kOptClenDy) != 0 && (Fout == 2 || Fout == 32 || Fout == 64) && M <= kGRT * 8 * 32 &&
          grp_clen_dy_lds(M, nnzT, K, Fout) <= size_t(kLdsBytes);
 }
 
@@ -947,10 +933,7 @@ hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* 
   if (Fin % kGQ || K < 1 || !grp_clen_dy_ok(M, nnzT, K, Fout))
     return hipErrorInvalidValue;
   const int G = Fin / kGQ;
-  static const int pipe = [] {  // CG_CLEN_DY=2: each group's tiles up front (A/B runs)
-    const char* e = getenv("CG_CLEN_DY");
-    return (e && e[0] == '2') ? 0 : 1;
-  }();
+  const int pipe = option(kOptClenDy) == 2 ? 0 : 1;  // 2: each group's tiles up front (A/B runs)
   GrpClenDyArgs a{trowptr, tcol, tval, order, M, rup(M + 1, 32), Fin, K, N, int(nnzT), G, Fout,
                   Fout / 2, dy, W, dx, dx_acc, pipe, nullptr};
 #ifdef CG_DEBUG

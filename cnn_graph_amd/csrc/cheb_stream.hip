@@ -1087,25 +1087,20 @@ int dw_chunks(int64_t R) {
 
 // the two-waves-per-SIMD build of the instantiations that fit in 256
 // registers: config C2's dW 223 -> 215 us, config E's weight-gradient pass
-// 584 -> 551 us (profiles/r04_j).  CG_DW_W2=0 keeps the one-wave build (A/B);
-// read per call
-static bool dw_two_waves() {
-  const char* e = getenv("CG_DW_W2");
-  return !(e && e[0] == '0');
-}
+// 584 -> 551 us (profiles/r04_j).  CG_OPT_DW_W2 = 0 keeps the one-wave build (A/B)
+static bool dw_two_waves() { return option(kOptDwW2) != 0; }
 
 // k_dw_direct for this shape, if one of its instantiations serves it: the dy
 // columns of the slice decide the B loads (VB, NLB), the basis columns (with
 // the LSTM's x-plane and ones columns) are cut into G groups of NA = VA*NLA
 // virtual tiles, NA chosen for the fewest MFMAs per row pair (G*NA*NB);
-// CG_DW_DIRECT=0 keeps k_dw_slabs (A/B runs); =2 forces k_dw_direct whatever
-// the wave count, =3 too but with one-float basis loads only (tests)
+// CG_OPT_DW_DIRECT = 0 keeps k_dw_slabs (A/B runs); 2 forces k_dw_direct
+// whatever the wave count, 3 too but with one-float basis loads only (tests)
 static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
                              int ldd, float* slab, hipStream_t s, int pl_fin, int64_t pl_stride,
                              int K, int chunks, int64_t rpc, const float* xb, int x_fin,
                              int64_t x_stride, hipError_t* err) {
-  const char* env = getenv("CG_DW_DIRECT");  // read per call: tests switch it in-process
-  const int mode = (env && env[0]) ? atoi(env) : 1;
+  const int mode = option(kOptDwDirect);
   if (mode == 0 || rpc < 256) return false;
   const bool a8 = (reinterpret_cast<uintptr_t>(basis) & 7) == 0;
   const bool b8 = (reinterpret_cast<uintptr_t>(dy) & 7) == 0;
@@ -1182,11 +1177,8 @@ static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int6
   }
   const size_t lds = size_t(kDwRB) * ((span | 1) + (((Fout + 31) & ~31) | 1)) * 4;
   const dim3 grid(chunks, groups);
-  // 8 waves per block unless CG_DW_WAVES=4 (A/B runs; the slabs are the same)
-  static const int nw = [] {
-    const char* e = getenv("CG_DW_WAVES");
-    return (e && e[0] == '4') ? 4 : 8;
-  }();
+  // 8 waves per block unless CG_OPT_DW_WAVES = 4 (A/B runs; the slabs are the same)
+  const int nw = option(kOptDwWaves);
   if (vw == 4 && nw == 8)
     hipLaunchKernelGGL((k_dw_slabs<4, 8>), grid, dim3(512), lds, s, basis, dy, R, FinK, Fout, rpc,
                        slab, pl_fin, pl_stride, K, tpb, xb, x_fin, x_stride, FinKh, ldd);

@@ -120,22 +120,7 @@ __device__ __forceinline__ void bst16_sc1(__amdgpu_buffer_rsrc_t r, int off, flo
   __builtin_amdgcn_raw_buffer_store_b128(w, r, off * 4, 0, 16);
 }
 
-// CG_SEQ_V=2: the decoupled kernel k_lstm_seq2 instead of k_lstm_seq (A/B runs;
-// the same outputs bitwise).  k_lstm_seq is the default: config E's layer
-// forward 1.29-1.31 ms against 1.74 ms for k_lstm_seq2 (profiles/r04_ab).
-// Read per launch.
-static bool seq_v2_enabled() {
-  const char* e = getenv("CG_SEQ_V");
-  return e && e[0] == '2';
-}
-
-static int seq_xpre() {
-  static const int on = [] {
-    const char* e = getenv("CG_SEQ_XPRE");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on;
-}
+static int seq_xpre() { return option(kOptSeqXpre); }
 
 struct SeqArgs {
   const int* rowptr;  // L~ (CSR, sorted columns)
@@ -168,7 +153,7 @@ struct SeqArgs {
   unsigned long long* ts;  // ablation build: phase stamps of step 1 (CG_TS), else NULL
   int xpre;           // 1: xplanes already hold T_k(x_t) for every step (launch_lstm_seq's
                       // pre-pass): the x contraction reads them, no x recurrence in the loop
-  int inject_t;       // fault injection (CG_SEQ_INJECT_HANG, tests only): >= 0 makes workgroup
+  int inject_t;       // fault injection (cg_plan_set_seq_fault_test, tests only): >= 0 makes workgroup
                       // 0 of pair 0 stop publishing its step counter from that step on
 };
 
@@ -600,377 +585,6 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
   }
 }
 
-// k_lstm_seq2: the same layer forward with the gate contraction DECOUPLED from
-// the recurrence -- bitwise the same hs / cs / act / planes as k_lstm_seq (the
-// same MFMA operand pairs in the same order for every accumulator):
-//   phase 1 (lockstep, LDS): the Chebyshev recurrence of the workgroup's own two
-//     8-channel quarters of h, T_1 .. T_{K-1} leaving as planes (write-through);
-//     no MFMA, so no accumulator is live and each lane keeps its rows' CSR
-//     columns packed in registers (lds_row_spmm_pc: a gather no longer waits
-//     on an LDS read of its column);
-//   hand-off: publish the step counter, wait for the partner's (as k_lstm_seq);
-//   phase 2 (free-running waves, no barrier): per 32-row tile (rows in natural
-//     order), load T_0 .. T_{K-1} of all four quarters from L2 (own planes and
-//     h included), contract on v_mfma_f32_32x32x2_f32 (x first, then quarters
-//     2u, 2u+1, then the partner's -- k_lstm_seq's order), then the gate update
-//     and the c / h / act stores of that tile right away.  Only one tile's 32
-//     accumulators are live (k_lstm_seq keeps 128 for 4 tiles through the whole
-//     step), so the next tile's operand loads are in flight during this tile's
-//     MFMAs, and one wave's gate math overlaps another's MFMAs.
-// KK = K: the orders one tile holds in registers; PF: the next tile's operands
-// loaded during this tile's MFMAs (off where its registers would spill)
-template <bool XPRE, int KK, bool PF>
-__global__ __launch_bounds__(kST) void k_lstm_seq2(SeqArgs A) {
-#pragma clang fp contract(off)
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ int s_abort;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j = lane & 31, hh = lane >> 5;
-  const int M = A.M, N = A.N, T = A.T;
-  constexpr int K = KK;
-  int pair, u;
-  if (A.pair_xcd) {
-    const int b = blockIdx.x;
-    pair = (b >> 4) * 8 + (b & 7);
-    u = (b >> 3) & 1;
-  } else {
-    pair = blockIdx.x >> 1;
-    u = blockIdx.x & 1;
-  }
-  float* slot0 = smem;
-  float* slot1 = smem + A.Mr * kQ;
-  float* s_W = slot1 + A.Mr * kQ;  // [K][q 4][s 4][hh 2][ct 2][i 32], as k_lstm_seq
-  float* s_Wx = s_W + K * 2048;
-  float* s_b = s_Wx + (A.xs ? K * 512 : 0);
-  float* s_val = s_b + 128;
-  unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
-  stage_lds<8, kST>(K * 2048, [&](int e) {
-    const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3;
-    const int q = (e >> 9) & 3, k = e >> 11;
-    const int ch = 8 * q + 4 * h2 + s;
-    const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
-    return A.Wh[int64_t(ch * K + k) * 128 + gcol];
-  }, [&](int e, float v) { s_W[e] = v; });
-  if (A.xs) {
-    stage_lds<8, kST>(K * 512, [&](int e) {
-      const int i = e & 31, ct = (e >> 5) & 1, h2 = (e >> 6) & 1, s = (e >> 7) & 3, k = e >> 9;
-      const int c = 2 * s + h2;
-      const int gcol = (i >> 3) * 32 + 16 * u + 8 * ct + (i & 7);
-      return c < A.Fin ? A.Wx[int64_t(c * K + k) * 128 + gcol] : 0.f;
-    }, [&](int e, float v) { s_Wx[e] = v; });
-  }
-  for (int e = tid; e < 128; e += kST) s_b[e] = A.bias ? A.bias[e] : 0.f;
-  for (int e = tid; e < A.nnz; e += kST) {
-    s_val[e] = A.val[e];
-    s_col[e] = static_cast<unsigned short>(A.col[e]);
-  }
-  if (tid == 0) s_abort = 0;
-  if (tid < 2 * kQ) (tid < kQ ? slot0 : slot1)[M * kQ + (tid & (kQ - 1))] = 0.f;  // zero row M
-  // phase-1 SpMM lanes: (row lane / 2, half lane % 2) over rows dealt by
-  // decreasing length (an 8-lane LDS access group gathers 4 whole records)
-  const int js = lane >> 1, hs2 = lane & 1;
-  int rowS[kRT], rb[kRT], re[kRT], wl[kRT];
-  bool rvS[kRT];
-#pragma unroll
-  for (int rt = 0; rt < kRT; ++rt) {
-    const int idxS = (wave + 8 * rt) * 32 + js;
-    rvS[rt] = idxS < M;
-    rowS[rt] = rvS[rt] ? A.order[idxS] : M;
-    rb[rt] = rvS[rt] ? A.rowptr[rowS[rt]] : 0;
-    re[rt] = rvS[rt] ? A.rowptr[rowS[rt] + 1] : 0;
-    wl[rt] = wave_max(re[rt] - rb[rt]);
-  }
-  // phase-2 / T_0 lanes: tile rt of the wave = rows (4 wave + rt) * 32 + j in
-  // natural order (row M -- the zero row -- past the graph)
-  int rN[kRT];
-  bool rv[kRT];
-#pragma unroll
-  for (int rt = 0; rt < kRT; ++rt) {
-    const int r = (4 * wave + rt) * 32 + j;
-    rv[rt] = r < M;
-    rN[rt] = rv[rt] ? r : M;
-  }
-  __syncthreads();
-  constexpr int NP = 6;  // packed columns: rows of up to 12 entries (longer: LDS columns)
-
-  int* my_flag = A.flags + 2 * pair + u;
-  const int* partner_flag = A.flags + 2 * pair + (1 - u);
-  for (int n = pair, it = 0; n < N; n += A.P, ++it) {
-    const int base = it * T;
-    for (int t = 0; t < T; ++t) {
-      const bool stamp = (t == 1 && it == 0);
-      if (stamp) CG_TS(A.ts, 0);
-      const bool has_h = t > 0 || A.h0;
-      const float* hsrc = (t == 0) ? A.h0 + int64_t(n) * M * kH
-                                   : A.hs + (int64_t(t - 1) * N + n) * M * kH;
-      float* pl_t = A.planes + (int64_t(t) * N + n) * M * kH;  // plane k at + (k-1)*pstride
-      const __amdgpu_buffer_rsrc_t r_hsrc = slab_rsrc(hsrc, M);
-      const __amdgpu_buffer_rsrc_t r_hout = slab_rsrc(A.hs + (int64_t(t) * N + n) * M * kH, M);
-      if (has_h) {
-        // phase 1: the recurrence of the OWN two quarters (units 16u .. 16u+15).
-        // The rows' CSR columns are packed into registers anew every step (a
-        // few LDS reads): held across phase 2 they would cost it 24 registers;
-        // the empty asm keeps the compiler from hoisting the packing out of
-        // the loop
-        asm volatile("" ::: "memory");
-        unsigned pk[kRT][NP];
-#pragma unroll
-        for (int rt = 0; rt < kRT; ++rt) pack_row_cols<NP>(pk[rt], s_col, rb[rt], re[rt], M);
-        for (int qq = 0; qq < 2; ++qq) {
-          const int q = 2 * u + qq;
-          float4 v[kRT];
-#pragma unroll
-          for (int rt = 0; rt < kRT; ++rt) {  // T_0 = h_{t-1}: this lane stored it (same row, units)
-            const int off = rN[rt] * kH + 8 * q + 4 * hh;
-            v[rt] = (t > 0) ? bld16_sc1(r_hsrc, off) : bld16(r_hsrc, off);
-          }
-#pragma unroll
-          for (int rt = 0; rt < kRT; ++rt)
-            *reinterpret_cast<float4*>(slot0 + rN[rt] * kQ + 4 * hh) = v[rt];
-          __syncthreads();
-          for (int k = 0; k + 1 < K; ++k) {
-            const float* cur = (k & 1) ? slot1 : slot0;
-            float* nxt = (k & 1) ? slot0 : slot1;
-#pragma unroll
-            for (int rt = 0; rt < kRT; ++rt) {
-              if (!rvS[rt] || CG_DBG(A.dbg, 2)) continue;
-              float4 sm;
-              with_row_len(wl[rt], [&](auto lc) {
-                constexpr int LL = decltype(lc)::value;
-                if constexpr (LL > 0 && LL <= 2 * NP)
-                  sm = lds_row_spmm_pc<LL, NP, 3>(cur, 4 * hs2, pk[rt], s_val, rb[rt], re[rt]);
-                else
-                  sm = lds_row_spmm_w<LL>(cur, kQ, 4 * hs2, s_col, s_val, rb[rt], re[rt], M);
-              });
-              float s0 = sm.x, s1 = sm.y, s2 = sm.z, s3 = sm.w;
-              float4* own = reinterpret_cast<float4*>(nxt + rowS[rt] * kQ + 4 * hs2);
-              if (k >= 1) {  // T_{k-1} of this row: the slot being overwritten
-                const float4 p = *own;
-                s0 = 2.f * s0 - p.x;
-                s1 = 2.f * s1 - p.y;
-                s2 = 2.f * s2 - p.z;
-                s3 = 2.f * s3 - p.w;
-              }
-              const float4 o = make_float4(s0, s1, s2, s3);
-              *own = o;
-              if (!CG_DBG(A.dbg, 32))
-                bst16_sc1(slab_rsrc(pl_t + int64_t(k) * A.pstride, M), rowS[rt] * kH + 8 * q + 4 * hs2, o);
-            }
-            __syncthreads();
-          }
-        }
-      }
-      if (stamp) CG_TS(A.ts, 1);
-      // publish: h_{t-1} of this workgroup's units (the previous step's phase 2)
-      // and the own quarters' planes of step t, drained; then the partner's
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0 && !(A.inject_t >= 0 && pair == 0 && u == 0 && base + t >= A.inject_t))
-        __hip_atomic_store(my_flag, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (has_h && !CG_DBG(A.dbg, 8)) {
-        if (tid == 0) {
-          const int need = base + t + 1;
-          const unsigned long long t0 = wall_clock64();
-          while (__hip_atomic_load(const_cast<int*>(partner_flag), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT) < need) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > A.timeout) {
-              s_abort = 1;
-              __hip_atomic_store(A.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              break;
-            }
-          }
-        }
-        __syncthreads();
-        if (s_abort) {  // every thread of the workgroup: poison what it owed, end
-          lstm_seq_poison(A, n, t, u);
-          return;
-        }
-      }
-      if (stamp) CG_TS(A.ts, 2);
-      // phase 2: per tile, all quarters' T_k from L2 -> MFMA -> gates -> stores.
-      // (a) this step's x basis values staged in slot0 as [row][k Fin + c]
-      // (phase 1 is done with the slots; rows past the graph read the zero
-      // row M), so no tile waits on a global x load
-      if (XPRE) {
-        const int Fin = A.Fin, MF = M * Fin;
-        const float* xp = A.xplanes + (int64_t(t) * N + n) * M * Fin;
-        stage_lds<8, kST>(K * MF, [&](int e) {
-          const int k = e / MF;
-          return xp[int64_t(k) * A.xpstride + (e - k * MF)];
-        }, [&](int e, float v) {
-          const int k = e / MF, rem = e - k * MF, row = rem / Fin;
-          slot0[row * kQ + k * Fin + (rem - row * Fin)] = v;
-        });
-        __syncthreads();
-      }
-      // (b) per tile: T_k of the four quarters and c_{t-1} loaded one tile ahead
-      // (buffer loads, a padding row reads 0); the weight operands of the next
-      // (quarter, order) group read from LDS ahead of the current group's MFMAs
-      const float* csrc = t > 0 ? A.cs + (int64_t(t - 1) * N + n) * M * kH
-                                : (A.c0 ? A.c0 + int64_t(n) * M * kH : A.cs);
-      const __amdgpu_buffer_rsrc_t r_c = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(csrc), 0, (t > 0 || A.c0) && !CG_DBG(A.dbg, 16) ? M * kH * 4 : 0,
-          0x00020000);
-      // the tile's graph row of this lane, M (the zero row) past the graph
-      auto row_n = [&](int rt) {
-        const int r = (4 * wave + rt) * 32 + j;
-        return r < M ? r : M;
-      };
-      struct TileOps {
-        float4 tk[4][KK];
-        float4 cv[2];
-      };
-      auto load_tile = [&](int rt, TileOps& o) {
-#pragma unroll
-        for (int qi = 0; qi < 4; ++qi) {
-          const int q = qi < 2 ? 2 * u + qi : 2 * (1 - u) + (qi - 2);
-#pragma unroll
-          for (int k = 0; k < KK; ++k) {
-            if (!has_h) continue;
-            const int off = row_n(rt) * kH + 8 * q + 4 * hh;
-            if (k == 0)
-              o.tk[qi][k] = t > 0 ? bld16_sc1(r_hsrc, off) : bld16(r_hsrc, off);
-            else
-              o.tk[qi][k] = bld16_sc1(slab_rsrc(pl_t + int64_t(k - 1) * A.pstride, M), off);
-          }
-        }
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) o.cv[ct] = bld16(r_c, row_n(rt) * kH + 16 * u + 8 * ct + 4 * hh);
-      };
-      // weight operands of group g = qi * KK + k: (s, ct) -> wq[s * 128 + ct * 32]
-      auto load_w = [&](int g, float (&w)[8]) {
-        const int qi = g / KK, k = g - qi * KK;
-        const int q = qi < 2 ? 2 * u + qi : 2 * (1 - u) + (qi - 2);
-        const float* wq = s_W + (k * 4 + q) * 512 + hh * 64 + j;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          w[2 * s] = wq[s * 128];
-          w[2 * s + 1] = wq[s * 128 + 32];
-        }
-      };
-      // a real loop over the tiles (unrolled, the scheduler mixes the tiles'
-      // registers and spills); PF: the next tile's loads are issued into a
-      // second register set before this tile's MFMAs, and moved over after
-      TileOps to, tn;
-      load_tile(0, to);
-#pragma unroll 1
-      for (int rt = 0; rt < kRT; ++rt) {
-        float4 (&tk)[4][KK] = to.tk;
-        if (PF && rt + 1 < kRT) load_tile(rt + 1, tn);  // in flight now
-        else if (!PF && rt > 0) load_tile(rt, to);
-        f32x16 acc[2];
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[ct][e] = 0.f;
-        if (XPRE) {
-          const int Fin = A.Fin;
-#pragma unroll
-          for (int k = 0; k < KK; ++k) {
-            const float* wq = s_Wx + k * 512 + hh * 64 + j;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              if (2 * s >= Fin || CG_DBG(A.dbg, 1)) break;
-              const int c = 2 * s + hh;
-              const float xv = slot0[row_n(rt) * kQ + k * Fin + (c < Fin ? c : 0)];
-              const float b = c < Fin ? xv : 0.f;
-              acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wq[s * 128], b, acc[0], 0, 0, 0);
-              acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wq[s * 128 + 32], b, acc[1], 0, 0, 0);
-            }
-          }
-        }
-        if (has_h && !CG_DBG(A.dbg, 1)) {
-          float w[2][8];
-          load_w(0, w[0]);
-#pragma unroll
-          for (int g = 0; g < 4 * KK; ++g) {
-            if (g + 1 < 4 * KK) load_w(g + 1, w[(g + 1) & 1]);
-            const int qi = g / KK, k = g - qi * KK;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-              const float b = (&tk[qi][k].x)[s];
-              acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[g & 1][2 * s], b, acc[0], 0, 0, 0);
-              acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[g & 1][2 * s + 1], b, acc[1], 0, 0, 0);
-            }
-            // the scheduler would otherwise hoist every group's weight reads
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-        // gate update of this tile: lane (row, hh) of tile ct holds gates g = 0..3
-        // of units 16u + 8ct + 4hh + m in acc[ct][4g + m]
-        if (row_n(rt) >= M) {
-          if (PF) to = tn;
-          continue;
-        }
-        const int64_t rr = (int64_t(t) * N + n) * M + row_n(rt);
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          const int u0 = 16 * u + 8 * ct + 4 * hh;
-          float4 gv[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            gv[g] = (CG_DBG(A.dbg, 16) || A.xs) ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                                : *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
-          const float4 cv = to.cv[ct];
-          float c[4] = {cv.x, cv.y, cv.z, cv.w};
-          float hn[4], zz[4], ii[4], ff[4], oo[4];
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const float gz = (&gv[0].x)[m], gi = (&gv[1].x)[m], gf = (&gv[2].x)[m],
-                        go = (&gv[3].x)[m];
-            float az = gz + acc[ct][m], ai = gi + acc[ct][4 + m];
-            float af = gf + acc[ct][8 + m], ao = go + acc[ct][12 + m];
-            if (A.bias) {
-              az = az + s_b[u0 + m];
-              ai = ai + s_b[32 + u0 + m];
-              af = af + s_b[64 + u0 + m];
-              ao = ao + s_b[96 + u0 + m];
-            }
-            float z, ig, fg, o, cn;
-            if (CG_DBG(A.dbg, 4)) {
-              z = az;
-              ig = ai;
-              fg = af;
-              o = ao;
-              cn = c[m] + az;
-              c[m] = cn;
-              hn[m] = ao * cn;
-            } else {
-              z = A.gates == 0 ? tanf(az) : tanhf(az);
-              ig = sigm(ai);
-              fg = sigm(af);
-              o = A.gates == 0 ? tanhf(ao) : sigm(ao);
-              cn = fg * c[m] + ig * z;
-              c[m] = cn;
-              hn[m] = o * tanhf(cn);
-            }
-            zz[m] = z;
-            ii[m] = ig;
-            ff[m] = fg;
-            oo[m] = o;
-          }
-          if (!CG_DBG(A.dbg, 128))
-            *reinterpret_cast<float4*>(A.cs + rr * kH + u0) = make_float4(c[0], c[1], c[2], c[3]);
-          if (!CG_DBG(A.dbg, 256))
-            bst16_sc1(r_hout, row_n(rt) * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
-          if (A.act && !CG_DBG(A.dbg, 64)) {
-            float* ap = A.act + rr * 128 + 4 * u0;
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-              *reinterpret_cast<float4*>(ap + 4 * m) = make_float4(zz[m], ii[m], ff[m], oo[m]);
-          }
-        }
-        if (PF) to = tn;
-      }
-      if (stamp) CG_TS(A.ts, 3);
-      // the next step's phase 1 reloads h into slot0, which holds this step's
-      // x values until every wave's phase 2 is done
-      if (XPRE) __syncthreads();
-    }
-  }
-}
-
 struct BStepArgs {
   const int* trowptr;  // L~^T (exact transpose, CSR)
   const int* tcol;
@@ -1272,7 +886,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   if (e != hipSuccess) return e;
   // x basis of all T steps up front (plane 0 = x, plane k = T_k(x) by the
   // streaming steps over the T*N samples: CSR order from +0, the same values
-  // as the in-loop recurrence), unless CG_SEQ_XPRE=0 (A/B runs): the loop
+  // as the in-loop recurrence), unless CG_OPT_SEQ_XPRE = 0 (A/B runs): the loop
   // then only contracts them, and neither workgroup of a pair recomputes them
   if (xs && seq_xpre()) {
     const int64_t R = int64_t(T) * N * M;
@@ -1295,25 +909,8 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   // other streams or processes can hold CUs, which is what the hand-off
   // timeout, the NaN poisoning and the plan's fault word are for
   const size_t lds = lstm_seq_lds(M, K, nnz, xs ? Fin : 0);
-  // k_lstm_seq2 (decoupled contraction) where it compiles without spills: the x
-  // basis precomputed (the default for feat_in <= 8) with K = 1 or 3, gx given
-  // with K = 1; the other shapes and the in-loop x recurrence (CG_SEQ_XPRE=0)
-  // keep k_lstm_seq
-  const bool v2 = seq_v2_enabled() && ((a.xpre && (K == 1 || K == 3)) || (!xs && K == 1));
-  const void* kern = nullptr;
-  if (!v2)
-    kern = a.xpre ? reinterpret_cast<const void*>(&k_lstm_seq<true>)
-                  : reinterpret_cast<const void*>(&k_lstm_seq<false>);
-  else if (!a.xpre)
-    kern = reinterpret_cast<const void*>(&k_lstm_seq2<false, 1, true>);
-  else if (K == 1)
-    kern = reinterpret_cast<const void*>(&k_lstm_seq2<true, 1, true>);
-  else
-    kern = reinterpret_cast<const void*>(&k_lstm_seq2<true, 3, false>);
-  if (v2) {
-    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes - kSeqStaticLds);
-    if (e != hipSuccess) return e;
-  }
+  const void* kern = a.xpre ? reinterpret_cast<const void*>(&k_lstm_seq<true>)
+                            : reinterpret_cast<const void*>(&k_lstm_seq<false>);
   int per_cu = 0, cus = 0;
   e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kST, lds);
   if (e != hipSuccess) return e;
@@ -1321,11 +918,8 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   if (e != hipSuccess) return e;
   if (per_cu < 1 || 2 * P > per_cu * cus) return hipErrorCooperativeLaunchTooLarge;
   const dim3 grid(2 * P), block(kST);
-  if (!v2 && a.xpre) hipLaunchKernelGGL(k_lstm_seq<true>, grid, block, lds, s, a);
-  else if (!v2) hipLaunchKernelGGL(k_lstm_seq<false>, grid, block, lds, s, a);
-  else if (!a.xpre) hipLaunchKernelGGL((k_lstm_seq2<false, 1, true>), grid, block, lds, s, a);
-  else if (K == 1) hipLaunchKernelGGL((k_lstm_seq2<true, 1, true>), grid, block, lds, s, a);
-  else hipLaunchKernelGGL((k_lstm_seq2<true, 3, false>), grid, block, lds, s, a);
+  if (a.xpre) hipLaunchKernelGGL(k_lstm_seq<true>, grid, block, lds, s, a);
+  else hipLaunchKernelGGL(k_lstm_seq<false>, grid, block, lds, s, a);
   return hipGetLastError();
 }
 

@@ -64,6 +64,12 @@ class ChebPlan:
         self.variant = variant
         self._shape_cache = {}
 
+    def set_seq_fault_test(self, step: int):
+        """Failure-detection test hook (cg_plan_set_seq_fault_test): from time step
+        ``step`` on, this plan's gconv-LSTM sequence launches lose one pair
+        hand-off; -1 turns it off."""
+        _lib.call("cg_plan_set_seq_fault_test", self._h, int(step))
+
     # workspaces above this size are not kept by the plan (a config-D backward
     # at N = 256 needs 51.5 GB: holding it for the plan's lifetime would pin it
     # for every later model that shares the plan through plan_for)

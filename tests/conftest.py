@@ -56,3 +56,18 @@ def golden():
             cache[name] = load_golden(name)
         return cache[name]
     return get
+
+
+@pytest.fixture
+def cg_opts():
+    """Set kernel-selection options (cg_set_option) for one test:
+    ``cg_opts("dw_direct", 0)``; every option touched is restored afterwards."""
+    from cnn_graph_amd import _lib
+    saved = {}
+
+    def setter(name, value):
+        prev = _lib.set_option(name, int(value))
+        saved.setdefault(name, prev)
+    yield setter
+    for name, prev in saved.items():
+        _lib.set_option(name, prev)

@@ -26,6 +26,29 @@ def test_release_library_has_no_ablation_hooks(built_lib):
     debug build (`make debug`); the shipping library must not export them."""
     h = _lib.lib()
     assert not hasattr(h, "cg_debug_set_flags")
+    # no environment switches or env-driven fault injection either: kernel
+    # choices go through cg_set_option, the hand-off fault test through the
+    # plan-scoped cg_plan_set_seq_fault_test
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for s in (b"getenv", b"CG_SEQ_INJECT_HANG", b"CG_SIDE_DW", b"CG_SEQ_V", b"k_lstm_seq2"):
+        assert s not in blob, s
+
+
+def test_options_roundtrip_and_validation(built_lib):
+    h = _lib.lib()
+    for name in _lib.OPTIONS:
+        v = _lib.get_option(name)
+        assert _lib.set_option(name, v) == v
+    assert _lib.get_option("dw_waves") == 8 and _lib.get_option("dw_direct") == 1
+    with _lib.options(dw_direct=0, clen_dy=2):
+        assert _lib.get_option("dw_direct") == 0 and _lib.get_option("clen_dy") == 2
+    assert _lib.get_option("dw_direct") == 1 and _lib.get_option("clen_dy") == 1
+    assert h.cg_set_option(99, 1) == _lib.CG_ERR_ARG
+    assert h.cg_set_option(_lib.OPTIONS["dw_waves"], 5) == _lib.CG_ERR_ARG
+    assert h.cg_set_option(_lib.OPTIONS["spmm_pw"], 2) == _lib.CG_ERR_ARG
+    assert h.cg_get_option(0, None) == _lib.CG_ERR_ARG
+    assert h.cg_plan_set_seq_fault_test(None, 1) == _lib.CG_ERR_ARG
 
 
 def test_plan_variant_validation(built_lib):

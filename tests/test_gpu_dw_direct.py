@@ -1,5 +1,5 @@
 """k_dw_direct (dW = basis^T dy on registers only, no LDS batches) against
-k_dw_slabs (CG_DW_DIRECT=0): the per-chunk slabs -- and so dW -- bitwise equal
+k_dw_slabs (CG_OPT_DW_DIRECT = 0): the per-chunk slabs -- and so dW -- bitwise equal
 (same chunks, same row pairs in the same order per output element, same MFMA),
 on the rows and planes layouts, every dy-width instantiation, ragged row
 counts and column tails; and dW within 1e-5 of float64.  Reference: the
@@ -25,15 +25,15 @@ def dev(built_lib):
 @pytest.mark.parametrize("R,FK,Fo", [(300001, 160, 32), (200003, 192, 64), (131072, 96, 128),
                                      (140001, 40, 256), (102400, 640, 32), (150000, 33, 30),
                                      (99999, 640, 2)])
-def test_dw_direct_rows_bitwise(dev, monkeypatch, R, FK, Fo):
+def test_dw_direct_rows_bitwise(dev, cg_opts, R, FK, Fo):
     from cnn_graph_amd import ops
     g = torch.Generator(device=dev)
     g.manual_seed(R + FK + Fo)
     A = torch.randn((R, FK), device=dev, generator=g)
     D = torch.randn((R, Fo), device=dev, generator=g)
-    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    cg_opts("dw_direct", "0")
     old = ops.weight_grad(A, D)
-    monkeypatch.setenv("CG_DW_DIRECT", "3")  # forced, whatever the wave count
+    cg_opts("dw_direct", "3")  # forced, whatever the wave count
     new = ops.weight_grad(A, D)
     torch.cuda.synchronize()
     assert torch.equal(new, old)
@@ -43,7 +43,7 @@ def test_dw_direct_rows_bitwise(dev, monkeypatch, R, FK, Fo):
 
 @pytest.mark.parametrize("mode", ["3", "2"])
 @pytest.mark.parametrize("R,Fin,K,Fo", [(200001, 64, 3, 64), (102400, 32, 20, 32), (80000, 16, 5, 128)])
-def test_dw_direct_planes_bitwise(dev, monkeypatch, mode, R, Fin, K, Fo):
+def test_dw_direct_planes_bitwise(dev, cg_opts, mode, R, Fin, K, Fo):
     from cnn_graph_amd import ops
     g = torch.Generator(device=dev)
     g.manual_seed(R + K)
@@ -51,9 +51,9 @@ def test_dw_direct_planes_bitwise(dev, monkeypatch, mode, R, Fin, K, Fo):
     buf = torch.randn((K * st,), device=dev, generator=g)
     D = torch.randn((R, Fo), device=dev, generator=g)
     planes = buf[:R * Fin].view(R, Fin)
-    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    cg_opts("dw_direct", "0")
     old = ops.weight_grad_planes(planes, st, K, R, D)
-    monkeypatch.setenv("CG_DW_DIRECT", mode)
+    cg_opts("dw_direct", mode)
     new = ops.weight_grad_planes(planes, st, K, R, D)
     torch.cuda.synchronize()
     assert torch.equal(new, old)
@@ -63,7 +63,7 @@ def test_dw_direct_planes_bitwise(dev, monkeypatch, mode, R, Fin, K, Fo):
 
 
 @pytest.mark.parametrize("R,Fin,K", [(12 * 8 * 1024, 2, 3), (50001, 1, 1), (40000, 8, 4)])
-def test_dw_direct_lstm_weight_grads_bitwise(dev, monkeypatch, R, Fin, K):
+def test_dw_direct_lstm_weight_grads_bitwise(dev, cg_opts, R, Fin, K):
     """cg_lstm_weight_grads' one pass (h planes, x planes and the ones column
     of the bias) on the direct kernel: dWh, dWx, db bitwise k_dw_slabs'."""
     from cnn_graph_amd import ops
@@ -75,9 +75,9 @@ def test_dw_direct_lstm_weight_grads_bitwise(dev, monkeypatch, R, Fin, K):
     xbuf = torch.randn((K * xst,), device=dev, generator=g)
     dpre = torch.randn((R, 4 * H), device=dev, generator=g)
     hpl, xpl = hbuf[:R * H].view(R, H), xbuf[:R * Fin].view(R, Fin)
-    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    cg_opts("dw_direct", "0")
     old = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
-    monkeypatch.setenv("CG_DW_DIRECT", "3")  # forced, whatever the wave count
+    cg_opts("dw_direct", "3")  # forced, whatever the wave count
     new = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
     torch.cuda.synchronize()
     for a, b in zip(new, old):
@@ -87,8 +87,8 @@ def test_dw_direct_lstm_weight_grads_bitwise(dev, monkeypatch, R, Fin, K):
 
 @pytest.mark.parametrize("R,FK,Fo", [(300001, 160, 32), (200003, 192, 64), (131072, 96, 128),
                                      (140001, 40, 256)])
-def test_dw_direct_two_waves_bitwise(dev, monkeypatch, R, FK, Fo):
-    """The two-waves-per-SIMD build (CG_DW_W2=1, <= 256 registers) against the
+def test_dw_direct_two_waves_bitwise(dev, cg_opts, R, FK, Fo):
+    """The two-waves-per-SIMD build (CG_OPT_DW_W2 = 1, <= 256 registers) against the
     one-wave build and k_dw_slabs: dW bitwise equal (same chunks, same pairs,
     same MFMA sequence per output)."""
     from cnn_graph_amd import ops
@@ -96,19 +96,19 @@ def test_dw_direct_two_waves_bitwise(dev, monkeypatch, R, FK, Fo):
     g.manual_seed(R + 7 * FK + Fo)
     A = torch.randn((R, FK), device=dev, generator=g)
     D = torch.randn((R, Fo), device=dev, generator=g)
-    monkeypatch.setenv("CG_DW_DIRECT", "0")
+    cg_opts("dw_direct", "0")
     ref = ops.weight_grad(A, D)
     out = {}
     for w2 in ("0", "1"):
-        monkeypatch.setenv("CG_DW_DIRECT", "3")
-        monkeypatch.setenv("CG_DW_W2", w2)
+        cg_opts("dw_direct", "3")
+        cg_opts("dw_w2", w2)
         out[w2] = ops.weight_grad(A, D)
     torch.cuda.synchronize()
     assert torch.equal(out["0"], ref)
     assert torch.equal(out["1"], ref)
 
 
-def test_dw_direct_two_waves_lstm_bitwise(dev, monkeypatch):
+def test_dw_direct_two_waves_lstm_bitwise(dev, cg_opts):
     """cg_lstm_weight_grads (config E's shape class: H 32, Fin 2, K 3) on the
     two-waves build: dWh, dWx, db bitwise the one-wave build's."""
     from cnn_graph_amd import ops
@@ -122,8 +122,8 @@ def test_dw_direct_two_waves_lstm_bitwise(dev, monkeypatch):
     hpl, xpl = hbuf[:R * H].view(R, H), xbuf[:R * Fin].view(R, Fin)
     out = {}
     for w2 in ("0", "1"):
-        monkeypatch.setenv("CG_DW_DIRECT", "3")
-        monkeypatch.setenv("CG_DW_W2", w2)
+        cg_opts("dw_direct", "3")
+        cg_opts("dw_w2", w2)
         out[w2] = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
     torch.cuda.synchronize()
     for a, b in zip(out["0"], out["1"]):

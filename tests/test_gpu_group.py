@@ -101,10 +101,10 @@ def test_group_clenshaw_fused_dx_accumulate(dev):
 
 
 @pytest.mark.parametrize("gname,N,Fin,K,Fout", [("golden_E.npz", 3, 32, 20, 24), ("golden_B.npz", 2, 16, 5, 40)])
-def test_group_clenshaw_packed_columns_bitwise(dev, monkeypatch, gname, N, Fin, K, Fout):
+def test_group_clenshaw_packed_columns_bitwise(dev, cg_opts, gname, N, Fin, K, Fout):
     """k_grp_clen (the dBasis-planes variant, Fout outside the fused kernel's
     2 / 32 / 64) with the rows' columns packed in registers (default) and read
-    from LDS every step (CG_GRP_PC=0): dx bitwise equal to each other and to
+    from LDS every step (CG_OPT_GRP_PC = 0): dx bitwise equal to each other and to
     the steps path."""
     from cnn_graph_amd import ops
     from cnn_graph_amd.plan import ChebPlan
@@ -117,7 +117,7 @@ def test_group_clenshaw_packed_columns_bitwise(dev, monkeypatch, gname, N, Fin, 
     dyt = _t(rng.standard_normal((N, M, Fout)), dev)
     out = {}
     for name, variant, pc in (("pc", "auto", "1"), ("lds", "auto", "0"), ("steps", "steps", "1")):
-        monkeypatch.setenv("CG_GRP_PC", pc)
+        cg_opts("grp_pc", pc)
         plan = ChebPlan(Lt, device=0, path="stream", variant=variant)
         r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
         r.forward(xt, Wt)
@@ -128,45 +128,11 @@ def test_group_clenshaw_packed_columns_bitwise(dev, monkeypatch, gname, N, Fin, 
     assert torch.equal(out["pc"], out["steps"])
 
 
-@pytest.mark.parametrize("layout", ["rows", "planes"])
-def test_group_side_stream_dw_bitwise(dev, monkeypatch, layout):
-    """dW on the plan's side stream, concurrent with k_grp_clen_dy
-    (CG_SIDE_DW=1) against dW in stream order after it (default): dx and
-    dW bitwise equal, and a read of dW right after the call on the caller's
-    stream sees the finished values (the join), over several back-to-back
-    calls that reuse the plan's fork / join events."""
-    from cnn_graph_amd import ops
-    from cnn_graph_amd.plan import ChebPlan
-    c = case(load_golden("golden_E.npz"))
-    M = c["M"]
-    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
-    N, Fin, K, Fout = 12, 32, 20, 32
-    rng = np.random.default_rng(77)
-    xt = _t(rng.standard_normal((N, M, Fin)), dev)
-    Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
-    dys = [_t(rng.standard_normal((N, M, Fout)), dev) for _ in range(3)]
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("CG_SIDE_DW", mode)
-        plan = ChebPlan(Lt, device=0, path="stream")
-        r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=layout)
-        r.forward(xt, Wt)
-        res = []
-        for dy in dys:
-            r.backward(dy, Wt)
-            res.append((r.dx.clone(), r.dW.clone()))  # clones on the caller's stream
-        torch.cuda.synchronize()
-        out[mode] = res
-    for (dx0, dW0), (dx1, dW1) in zip(out["0"], out["1"]):
-        assert torch.equal(dx0, dx1)
-        assert torch.equal(dW0, dW1)
-
-
 @pytest.mark.parametrize("gname,N,Fin,K,Fout", [("golden_E.npz", 3, 32, 20, 32), ("golden_B.npz", 2, 16, 5, 32),
                                                 ("golden_B.npz", 2, 32, 7, 20)])
-def test_group_fwd_paired_metadata_bitwise(dev, monkeypatch, gname, N, Fin, K, Fout):
+def test_group_fwd_paired_metadata_bitwise(dev, cg_opts, gname, N, Fin, K, Fout):
     """k_grp16_fwd with the CSR metadata read two entries per LDS access
-    (lds_row_spmm_w, default) against one per access (CG_SPMM_PW=0): basis
+    (lds_row_spmm_w, default) against one per access (CG_OPT_SPMM_PW = 0): basis
     planes and y bitwise equal (rows start at both parities of the CSR)."""
     from cnn_graph_amd import ops
     from cnn_graph_amd.plan import ChebPlan
@@ -179,7 +145,7 @@ def test_group_fwd_paired_metadata_bitwise(dev, monkeypatch, gname, N, Fin, K, F
     Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
     out = {}
     for pw in ("1", "0"):
-        monkeypatch.setenv("CG_SPMM_PW", pw)
+        cg_opts("spmm_pw", pw)
         plan = ChebPlan(Lt, device=0, path="stream")
         r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="planes")
         r.forward(xt, Wt)
