@@ -303,6 +303,15 @@ def pmc_mfma_busy(kernel, cfg):
     return round(busy_us / k["avg_us"], 4), d.get("source")
 
 
+def max_over_ranks(vals, dev):
+    """Element-wise MAX of host floats over the ranks (a device tensor on
+    nccl = RCCL, a host tensor on gloo)."""
+    on_dev = dist.get_backend() == "nccl"
+    tt = torch.tensor(vals, dtype=torch.float64, device=dev if on_dev else "cpu")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return [float(v) for v in tt.tolist()]
+
+
 def spawn_ranks(n):
     """Re-launch this command under torchrun with n ranks (one per GPU) as a
     CHILD process -- nothing here has touched the GPU -- and return its status."""
@@ -341,7 +350,14 @@ def main():
                     help="capture the K timed steps into one HIP graph before the timed region and "
                          "replay it there (every kernel of every step still runs); measured 0-1 %% "
                          "slower than eager launches on config B (profiles/r03_graph), so off")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "gloo"],
+                    help="test only: gloo runs the N > 1 entry path (torchrun, init, barrier, max over "
+                         "ranks) with every rank on GPU local_rank mod the visible GPUs, e.g. two "
+                         "ranks on a one-GPU box (needs --allreduce torch: RCCL refuses two ranks "
+                         "on one device); auto = nccl (RCCL) whenever a GPU is visible")
     args = ap.parse_args()
+    if args.dist_backend == "gloo" and args.allreduce != "torch":
+        sys.exit("bench.py: --dist-backend gloo needs --allreduce torch")
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
@@ -354,7 +370,9 @@ def main():
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
-    rank, world, local = cdist.init()
+    rank, world, local = cdist.init("gloo" if args.dist_backend == "gloo" else None)
+    if args.dist_backend == "gloo":
+        local %= torch.cuda.device_count()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -401,8 +419,10 @@ def main():
             if st:
                 _lib.check("cg_allreduce_sum_f32", st)
     elif exchange:
+        tcomm = cdist.TorchComm()  # ProcessGroupNCCL on RCCL, a host copy on gloo
+
         def allreduce(s):
-            dist.all_reduce(runner.dW, op=dist.ReduceOp.SUM)
+            tcomm.allreduce_sum_(runner.dW)
 
     # The step schedule (cnn_graph_amd/dp_step.py, driven at world 2 by
     # tests/test_gpu_dp_bench.py): with no exchange step (one GPU) the Adam
@@ -473,9 +493,7 @@ def main():
         raise
     check_comm()
     if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed, = max_over_ranks([elapsed], dev)
 
     # per-step distribution (SURVEY.md §8d asks for the median step): a second
     # pass of the same steps with a HIP event between consecutive steps on
@@ -494,9 +512,7 @@ def main():
     med_ms = float(np.median(per_step))
     p90_ms = float(np.percentile(per_step, 90))
     if world > 1:
-        tt = torch.tensor([med_ms, p90_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        med_ms, p90_ms = (float(v) for v in tt.tolist())
+        med_ms, p90_ms = max_over_ranks([med_ms, p90_ms], dev)
 
     # per-kernel timing (roofline.achieved), on the warm GPU: forward = one
     # kernel; backward = the recurrence kernel + the tiny fixed-order dW slab reduce
@@ -545,6 +561,7 @@ def main():
                    "Fin": Fin, "Fout": Fout, "path": path, "basis_layout": runner.basis_layout,
                    "parallelism": f"dp{world}",
                    "allreduce": (args.allreduce if exchange else None),
+                   "dist_backend": (dist.get_backend() if world > 1 else None),
                    "rccl_nranks": rccl_nranks,
                    "launch": ("one HIP graph replay of the K captured steps" if graph is not None
                               else "eager C-ABI calls per step"),

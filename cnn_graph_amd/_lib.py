@@ -139,6 +139,9 @@ _SIGNATURES = {
                                _c_i32, ctypes.c_float, _vp, _c_sz, _vp], _c_int),
     "cg_adam_update": ([_vp, _vp, _vp, _vp, _c_i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                         ctypes.c_float, _c_i32, ctypes.c_float, _vp], _c_int),
+    "cg_sgd_update": ([_vp, _vp, _c_i64, ctypes.c_float, ctypes.c_float, _vp], _c_int),
+    "cg_rmsprop_update": ([_vp, _vp, _vp, _vp, _c_i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                           ctypes.c_float, ctypes.c_float, _vp], _c_int),
     "cg_comm_unique_id": ([ctypes.c_char_p], _c_int),
     "cg_comm_init": ([ctypes.POINTER(_vp), _c_int, _c_int, ctypes.c_char_p, _c_int], _c_int),
     "cg_allreduce_sum_f32": ([_vp, _vp, _c_sz, _vp], _c_int),

@@ -431,6 +431,10 @@ hipError_t launch_maxpool_bwd(const float* dy, const int32_t* arg, int N, int M,
 hipError_t launch_avgpool_fwd(const float* x, int N, int M, int F, int p, float* y, hipStream_t s);
 hipError_t launch_avgpool_bwd(const float* dy, int N, int M, int F, int p, float* dx,
                               hipStream_t s);
+hipError_t launch_sgd(float* param, const float* grad, int64_t n, float lr, float grad_scale,
+                      hipStream_t s);
+hipError_t launch_rmsprop(float* param, const float* grad, float* ms, float* mom, int64_t n, float lr,
+                          float rho, float momentum, float eps, float grad_scale, hipStream_t s);
 hipError_t launch_adam(float* param, const float* grad, float* m, float* v, int64_t n, float lr_t,
                        float beta1, float beta2, float eps, float grad_scale, hipStream_t s);
 // One Adam step applied by the slab reduction that produces its gradient.

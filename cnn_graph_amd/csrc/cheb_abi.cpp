@@ -796,7 +796,7 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
   float* slots = static_cast<float*>(workspace);
   const size_t slot = size_t(M) * size_t(N) * size_t(Fin);
   if (K == 1) {
-    CG_HIP(hipMemcpyAsync(basis, x, slot * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (x != basis) CG_HIP(hipMemcpyAsync(basis, x, slot * sizeof(float), hipMemcpyDeviceToDevice, s));
   } else if (w.wide) {
     // wide columns: T_0 = x re-laid [M][Fin*N] into plane 0, the K-1 steps
     // plane to plane, then the basis (lib/graph_conv.py:155-172)
@@ -825,11 +825,12 @@ int forward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout,
                               W, basis, static_cast<float*>(workspace), res, act, y, s));
     return ok();
   } else if (layout == CG_BASIS_PLANES) {
-    // planes layout: T_k IS plane k of the basis (plane 0 a copy of x), every
-    // step writes its own plane, no assembly step (lib/graph_conv.py:159-169)
+    // planes layout: T_k IS plane k of the basis (plane 0 = x: copied unless
+    // the caller placed x there), every step writes its own plane, no assembly
+    // step (lib/graph_conv.py:159-169)
     const int* rperm = (Fin >= 16) ? plan->rperm : nullptr;
     auto P = [&](int k) { return basis + size_t(k) * slot; };
-    CG_HIP(hipMemcpyAsync(basis, x, slot * sizeof(float), hipMemcpyDeviceToDevice, s));
+    if (x != basis) CG_HIP(hipMemcpyAsync(basis, x, slot * sizeof(float), hipMemcpyDeviceToDevice, s));
     for (int k = 1; k < K; ++k)
       CG_HIP(cg::launch_cheb_step(plan->rowptr, plan->col, plan->val, rperm, k == 1 ? x : P(k - 1),
                                   k == 2 ? x : (k > 2 ? P(k - 2) : nullptr), P(k), x, nullptr,
@@ -1808,6 +1809,24 @@ int cg_adam_update(float* param, const float* grad, float* m, float* v, int64_t 
       double(lr) * std::sqrt(1.0 - std::pow(double(beta2), step)) / (1.0 - std::pow(double(beta1), step));
   CG_HIP(cg::launch_adam(param, grad, m, v, n, float(lr_t), beta1, beta2, eps, grad_scale,
                          reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_sgd_update(float* param, const float* grad, int64_t n, float lr, float grad_scale,
+                  void* stream) {
+  if (!param || !grad || n < 0) return fail(CG_ERR_ARG, "sgd_update: bad arguments");
+  if (n == 0) return ok();
+  CG_HIP(cg::launch_sgd(param, grad, n, lr, grad_scale, reinterpret_cast<hipStream_t>(stream)));
+  return ok();
+}
+
+int cg_rmsprop_update(float* param, const float* grad, float* ms, float* mom, int64_t n, float lr,
+                      float rho, float momentum, float eps, float grad_scale, void* stream) {
+  if (!param || !grad || !ms || !mom || n < 0 || !(eps > 0.f))
+    return fail(CG_ERR_ARG, "rmsprop_update: bad arguments");
+  if (n == 0) return ok();
+  CG_HIP(cg::launch_rmsprop(param, grad, ms, mom, n, lr, rho, momentum, eps, grad_scale,
+                            reinterpret_cast<hipStream_t>(stream)));
   return ok();
 }
 

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
     if (rvS[rt]) {
       const int64_t o = (int64_t(n) * M + rowS[rt]) * Fin + c0;
       const float4 v = *reinterpret_cast<const float4*>(A.x + o);
-      *reinterpret_cast<float4*>(A.basis + o) = v;  // plane 0 = x
+      if (A.x != A.basis) *reinterpret_cast<float4*>(A.basis + o) = v;  // plane 0 = x (unless x IS it)
       *reinterpret_cast<float4*>(slot0 + rowS[rt] * kGQ + 4 * hs) = v;
     }
   }
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
       if (rvS[rt][hf]) {
         const int64_t o = (int64_t(n) * M + rowS[rt][hf]) * Fin + c0;
         const float4 v = *reinterpret_cast<const float4*>(A.x + o);
-        *reinterpret_cast<float4*>(A.basis + o) = v;  // plane 0 = x
+        if (A.x != A.basis) *reinterpret_cast<float4*>(A.basis + o) = v;  // plane 0 = x (unless x IS it)
         *reinterpret_cast<float4*>(slot + rowS[rt][hf] * kGQ16 + 4 * qs) = v;
       }
     }

@@ -128,6 +128,39 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ param,
     adam_elem(param, m, v, i, grad[i], grad_scale, lr_t, beta1, beta2, eps);
 }
 
+// The other update rules of gconvRNN.Model._build_optim (lib/gconvRNN.py:381-389)
+// with TF 1.x's kernels (training_ops.cc), grad * grad_scale first:
+//   GradientDescent (ApplyGradientDescent): p -= g lr
+//   RMSProp (ApplyRMSProp, not centered):   ms += (g^2 - ms)(1 - rho)
+//                                           mom = mom momentum + (g lr) / sqrt(ms + eps)
+//                                           p -= mom
+__global__ __launch_bounds__(256) void k_sgd(float* __restrict__ param, const float* __restrict__ grad,
+                                             int64_t n, float lr, float grad_scale) {
+#pragma clang fp contract(off)
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const float g = grad[i] * grad_scale;
+    param[i] = param[i] - g * lr;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rmsprop(float* __restrict__ param,
+                                                 const float* __restrict__ grad,
+                                                 float* __restrict__ ms, float* __restrict__ mom,
+                                                 int64_t n, float lr, float rho, float momentum,
+                                                 float eps, float grad_scale) {
+#pragma clang fp contract(off)
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const float g = grad[i] * grad_scale;
+    const float s = ms[i] + (g * g - ms[i]) * (1.f - rho);
+    const float u = mom[i] * momentum + (g * lr) / sqrtf(s + eps);
+    ms[i] = s;
+    mom[i] = u;
+    param[i] = param[i] - u;
+  }
+}
+
 // Slab reduction + Adam for a step with no exchange between them (one GPU):
 // the summation is k_reduce_slabs' (wave w sums slabs w, w+16, ..., then the 16
 // partials in wave order), so grad is bitwise the unfused dW; wave 0 then
@@ -221,6 +254,19 @@ hipError_t launch_adam(float* param, const float* grad, float* m, float* v, int6
                        float beta1, float beta2, float eps, float grad_scale, hipStream_t s) {
   hipLaunchKernelGGL(k_adam, dim3(grid_for(n, 256)), dim3(256), 0, s, param, grad, m, v, n, lr_t,
                      beta1, beta2, eps, grad_scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_sgd(float* param, const float* grad, int64_t n, float lr, float grad_scale,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_sgd, dim3(grid_for(n, 256)), dim3(256), 0, s, param, grad, n, lr, grad_scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_rmsprop(float* param, const float* grad, float* ms, float* mom, int64_t n, float lr,
+                          float rho, float momentum, float eps, float grad_scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_rmsprop, dim3(grid_for(n, 256)), dim3(256), 0, s, param, grad, ms, mom, n, lr,
+                     rho, momentum, eps, grad_scale);
   return hipGetLastError();
 }
 

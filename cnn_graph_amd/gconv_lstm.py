@@ -11,9 +11,19 @@ Reference behaviour kept:
     -- ``gates="standard"`` gives the usual tanh / sigmoid instead;
   * ``forget_bias`` is accepted and ignored, as in the reference (:49);
   * ``__call__(inputs, state) -> (new_h, LSTMStateTuple(new_c, new_h))``.
-  * ``DropoutWrapper(output_keep_prob=0.8)`` (:616, :623) is NOT applied: it is
-    training-time noise outside the filter path (pass ``keep_prob`` to
-    ``static_rnn`` callers' own dropout if needed).
+  * ``DropoutWrapper(cell, output_keep_prob)`` (:616, :623): the cell's outputs
+    go through ``tf.nn.dropout`` on a HIP kernel (``ops.dropout``); every
+    wrapper draws its own mask stream (a distinct seed per wrapper unless one
+    is given), as each TF DropoutWrapper owns an independent random op.
+  * ``GLSTMModel``: ``inference_glstm`` (:271-281) -- glstm_layer, the last
+    step's output, ``fc_layer`` (:629-636) -- with the MSE loss and the
+    optimizer step (lib/graph_model.py:246-310; sgd / rmsprop of
+    lib/gconvRNN.py:381-389), data parallel with ONE all-reduce of a flat
+    gradient bucket per step (config E: batch 512 over 4 GPUs).
+
+Run validation / inference under ``torch.no_grad()``: with gradients enabled a
+lost pair hand-off of the one-launch layer is reported when the backward runs
+(or at the next layer() call on the plan), not before the forward returns.
 
 MI355X design: the four x-weights (and the four h-weights) are stored
 concatenated as one [K*F, 4H] matrix, so a cell step is ONE x-conv plus ONE
@@ -34,8 +44,16 @@ import math
 
 import torch
 
+import ctypes
+import itertools
+
+from . import _lib
 from . import ops
+from .graph_conv import truncated_normal_
 from .plan import plan_for
+
+# distinct default mask streams per DropoutWrapper (TF: one random op each)
+_DROPOUT_ORDINAL = itertools.count(1)
 
 _LSTMStateTuple = collections.namedtuple("LSTMStateTuple", ("c", "h"))
 
@@ -382,13 +400,17 @@ class DropoutWrapper:
     the reference graph, it drops whenever it is applied (there is no training
     flag); output_keep_prob = 1 is the identity.  The mask stream is seeded
     from ``seed`` and advances every call (TF's own random stream is not
-    reproducible here, only its semantics)."""
+    reproducible here, only its semantics).  With ``seed=None`` every wrapper
+    gets its own stream (torch.initial_seed() mixed with the wrapper's creation
+    ordinal), so two same-shaped layers never share masks."""
 
-    def __init__(self, cell: GConvLSTMCell, output_keep_prob: float = 1.0, seed: int = 0):
+    def __init__(self, cell: GConvLSTMCell, output_keep_prob: float = 1.0, seed: int | None = None):
         if not 0.0 < float(output_keep_prob) <= 1.0:
             raise ValueError(f"output_keep_prob must be in (0, 1], got {output_keep_prob}")
         self.cell = cell
         self.output_keep_prob = float(output_keep_prob)
+        if seed is None:
+            seed = (torch.initial_seed() * 0x9E3779B97F4A7C15 + next(_DROPOUT_ORDINAL) * 0xBF58476D1CE4E5B9)
         self._seed = int(seed) & ((1 << 64) - 1)
         self._calls = 0
 
@@ -397,6 +419,10 @@ class DropoutWrapper:
         return (self._seed + 0xD1B54A32D192ED03 * self._calls) & ((1 << 64) - 1)
 
     def __getattr__(self, name):  # state_size, output_size, zero_state, parameters, ...
+        # only reached for names not found normally; 'cell' itself missing means
+        # an instance built without __init__ (copy / pickle probing): no recursion
+        if name == "cell" or name.startswith("__"):
+            raise AttributeError(name)
         return getattr(self.cell, name)
 
     def __call__(self, inputs, state, scope=None):
@@ -466,3 +492,164 @@ def unstack_time(x: torch.Tensor, T: int) -> torch.Tensor:
     reshape [N, M, F, T] -> unstack axis 3 -> [T, N, M, F] (contiguous)."""
     N, M, C = x.shape
     return x.reshape(N, M, C // T, T).permute(3, 0, 1, 2).contiguous()
+
+
+class GLSTMModel:
+    """``GconvModel.inference_glstm`` (lib/gconv_lstm.py:271-281) trained as
+    ``GraphModel`` trains it (lib/graph_model.py:246-310):
+
+      x [N, M, F*T]  --unstack time (:272-275)-->  T x [N, M, F]
+      glstm_layer    layer_count GConvLSTMCells under static_rnn (:609-627),
+                     each in a DropoutWrapper(output_keep_prob) (:616, :623)
+      fc_layer       out = cheby_conv(outputs[-1]; W_fc [K*H, Fout]) (:629-636)
+      loss           mean((labels - out)^2) + its moving average    cg_mse_loss_ema
+      exchange       ONE all-reduce(sum) of the flat gradient bucket (N > 1)
+      update         ONE optimizer launch over the flat parameter buffer,
+                     grad_scale = 1/world: Adam (graph_model.py:293, staircase
+                     exponential decay) or gconvRNN's sgd / rmsprop
+                     (lib/gconvRNN.py:381-389)
+
+    Every parameter (each layer's Wx [K*Fin, 4H], Wh [K*H, 4H], b [4H], then
+    W_fc) is a view into one flat fp32 buffer and its ``.grad`` a view into one
+    flat gradient bucket that autograd accumulates into in place -- at config E
+    (Fin 2, H 32, K 3, one layer) 13 376 floats = 53.5 KB -- so the data-parallel
+    exchange of a step is one collective and the update one launch.
+    ``comm`` is any object with ``allreduce_sum_(tensor, stream)`` and ``world``
+    (``dist.RcclComm`` on RCCL, ``dist.TorchComm`` on a process group)."""
+
+    OPTIMIZERS = ("adam", "sgd", "rmsprop")
+
+    def __init__(self, L, N: int, T: int, feat_in: int, num_hidden: int = 32, K: int = 3,
+                 layer_count: int = 1, out_features: int = 2, keep_prob: float = 0.8,
+                 optimizer: str = "adam", learning_rate: float = 1e-3, decay_rate: float = 0.95,
+                 decay_steps: int | None = None, lmax: float = 2, gates: str = "reference",
+                 device=None, seed: int = 2017, comm=None):
+        if optimizer not in self.OPTIMIZERS:
+            raise ValueError(f"optimizer must be one of {self.OPTIMIZERS}")
+        self.device = torch.device(device if device is not None else "cuda")
+        self.N, self.T, self.F, self.H, self.K = int(N), int(T), int(feat_in), int(num_hidden), int(K)
+        self.Fout = int(out_features)
+        self.optimizer, self.lr = optimizer, learning_rate
+        self.decay_rate, self.decay_steps = decay_rate, decay_steps
+        self.comm = comm
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed)
+        cells = []
+        for li in range(int(layer_count)):
+            fin = self.F if li == 0 else self.H
+            cells.append(GConvLSTMCell(self.H, laplacian=L, lmax=lmax, K=self.K, feat_in=fin,
+                                       gates=gates, device=self.device, generator=gen))
+        self.plan = cells[0].plan
+        self.M = self.plan.M
+        H, K = self.H, self.K
+        sizes = [c.Wx.numel() + c.Wh.numel() + c.b.numel() for c in cells] + [K * H * self.Fout]
+        f32 = dict(device=self.device, dtype=torch.float32)
+        total = sum(sizes)
+        self.flat = torch.empty(total, **f32)
+        self.grad = torch.zeros(total, **f32)
+        self.names, self.params = [], []
+        off = 0
+
+        def bind(t_init, name):
+            nonlocal off
+            n = t_init.numel()
+            view = self.flat[off:off + n].view_as(t_init)
+            view.copy_(t_init)
+            p = torch.nn.Parameter(view)   # aliases the flat buffer
+            p.grad = self.grad[off:off + n].view_as(t_init)
+            off += n
+            self.names.append(name)
+            self.params.append(p)
+            return p
+
+        scope = "gconv_lstm_layer/rnn/multi_rnn_cell/cell_{}/"
+        for li, c in enumerate(cells):
+            with torch.no_grad():
+                c.Wx = bind(c.Wx.detach(), scope.format(li) + "Wx")
+                c.Wh = bind(c.Wh.detach(), scope.format(li) + "Wh")
+                c.b = bind(c.b.detach(), scope.format(li) + "b")
+        with torch.no_grad():
+            w0 = truncated_normal_(torch.empty((K * H, self.Fout), **f32), 0.1, gen)
+            self.W_fc = bind(w0, "conv_init/weights")
+        assert off == total
+        self.cells = cells
+        self.wrapped = [DropoutWrapper(c, keep_prob) if keep_prob < 1.0 else c for c in cells]
+        # optimizer slots (TF 1.x: Adam m, v zeros; RMSProp ms ONES, mom zeros)
+        self.s1 = (torch.ones if optimizer == "rmsprop" else torch.zeros)(total, **f32)
+        self.s2 = torch.zeros(total, **f32)
+        self.loss = torch.empty((1,), **f32)
+        self.ema = torch.zeros((3,), **f32)  # ExponentialMovingAverage(0.9) of the loss
+        self.dout = torch.empty((self.N, self.M, self.Fout), **f32)
+        nb = ctypes.c_size_t()
+        _lib.call("cg_mse_loss_workspace_bytes", self.N * self.M * self.Fout, ctypes.byref(nb))
+        self.mws = torch.empty(max(nb.value, 1), device=self.device, dtype=torch.uint8)
+        self.mws_n = nb.value
+        self.step_count = 0
+
+    @property
+    def world(self):
+        return self.comm.world if self.comm is not None else 1
+
+    @property
+    def loss_average(self):
+        return self.ema[1:2]
+
+    def parameters(self):
+        return dict(zip(self.names, self.params))
+
+    def gradients(self):
+        return dict(zip(self.names, (p.grad for p in self.params)))
+
+    def learning_rate(self, step):
+        """tf.train.exponential_decay(lr, global_step, decay_steps, decay_rate, staircase=True)."""
+        if self.decay_rate == 1 or not self.decay_steps:
+            return self.lr
+        return self.lr * self.decay_rate ** math.floor(step / self.decay_steps)
+
+    def _steps(self, x):
+        if x.dim() == 3:  # [N, M, F*T] as the reference feeds it
+            return unstack_time(x, self.T)
+        return x.contiguous()
+
+    def forward(self, x):
+        """inference_glstm: the fc layer's output [N, M, out_features]."""
+        outs, _ = static_rnn(self.wrapped, self._steps(x))
+        return ops.cheb_conv(outs[-1].contiguous(), self.W_fc, self.plan, self.K)
+
+    def train_step(self, x, labels, stream=None):
+        """One optimizer step; returns the device loss [1] (this rank's batch)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        self.grad.zero_()
+        out = self.forward(x)
+        labels = labels.contiguous()
+        if labels.numel() != out.numel():
+            raise ValueError("labels must match the logits' shape")
+        _lib.call("cg_mse_loss_ema", out.data_ptr(), labels.data_ptr(), out.numel(),
+                  self.loss.data_ptr(), self.dout.data_ptr(), self.ema.data_ptr(),
+                  ctypes.c_float(0.9), self.mws.data_ptr(), self.mws_n, s)
+        out.backward(self.dout)
+        for p in self.params:  # autograd accumulated into the flat bucket in place
+            if p.grad is None or p.grad.data_ptr() < self.grad.data_ptr() or \
+                    p.grad.data_ptr() >= self.grad.data_ptr() + 4 * self.grad.numel():
+                raise RuntimeError("a parameter's .grad left the flat gradient bucket")
+        world = 1
+        if self.comm is not None and self.comm.world > 1:
+            self.comm.allreduce_sum_(self.grad, s)
+            world = self.comm.world
+        self.step_count += 1
+        lr = self.learning_rate(self.step_count - 1)
+        n = self.flat.numel()
+        if self.optimizer == "adam":
+            _lib.call("cg_adam_update", self.flat.data_ptr(), self.grad.data_ptr(), self.s1.data_ptr(),
+                      self.s2.data_ptr(), n, ctypes.c_float(lr), ctypes.c_float(0.9),
+                      ctypes.c_float(0.999), ctypes.c_float(1e-8), self.step_count,
+                      ctypes.c_float(1.0 / world), s)
+        elif self.optimizer == "sgd":
+            _lib.call("cg_sgd_update", self.flat.data_ptr(), self.grad.data_ptr(), n,
+                      ctypes.c_float(lr), ctypes.c_float(1.0 / world), s)
+        else:
+            _lib.call("cg_rmsprop_update", self.flat.data_ptr(), self.grad.data_ptr(),
+                      self.s1.data_ptr(), self.s2.data_ptr(), n, ctypes.c_float(lr),
+                      ctypes.c_float(0.9), ctypes.c_float(0.0), ctypes.c_float(1e-10),
+                      ctypes.c_float(1.0 / world), s)
+        return self.loss

@@ -229,6 +229,15 @@ class ChebRunner:
         self._fwd = _lib.lib().cg_cheb_forward_layout
         self._bwd = _lib.lib().cg_cheb_backward_layout
 
+    def input_plane(self) -> torch.Tensor | None:
+        """Planes layout: plane 0 of the saved basis as an [N, M, Fin] tensor.  A
+        producer that writes the filter input there (and passes it as x) saves
+        the forward's copy of x into plane 0 (cg_cheb_forward_layout reads
+        T_0 in place when x == basis).  None for the other layouts."""
+        if self.basis_layout != "planes":
+            return None
+        return self.basis[0].view(self.N, self.plan.M, self.Fin)
+
     def basis_rows(self) -> torch.Tensor:
         """The saved basis as [N*M, Fin*K] (a copy when the layout is 'orders')."""
         if self.basis_layout == "rows":
@@ -867,6 +876,28 @@ def adam_update(param, grad, m, v, step: int, lr=1e-3, beta1=0.9, beta2=0.999, e
             raise ValueError(f"{name} must be contiguous")
     _lib.call("cg_adam_update", _p(param), _p(grad), _p(m), _p(v), param.numel(), float(lr),
               float(beta1), float(beta2), float(eps), int(step), float(grad_scale), _stream(param))
+
+
+def sgd_update(param, grad, lr=1e-3, grad_scale=1.0):
+    """In-place tf.train.GradientDescentOptimizer step (lib/gconvRNN.py:383-384)."""
+    for name, t in (("param", param), ("grad", grad)):
+        _check_dev(name, t)
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+    _lib.call("cg_sgd_update", _p(param), _p(grad), param.numel(), float(lr), float(grad_scale),
+              _stream(param))
+
+
+def rmsprop_update(param, grad, ms, mom, lr=1e-3, rho=0.9, momentum=0.0, eps=1e-10,
+                   grad_scale=1.0):
+    """In-place tf.train.RMSPropOptimizer step (lib/gconvRNN.py:387-388; TF 1.x
+    ApplyRMSProp, not centered).  ms starts at ONES, mom at zeros (TF 1.x slots)."""
+    for name, t in (("param", param), ("grad", grad), ("ms", ms), ("mom", mom)):
+        _check_dev(name, t)
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+    _lib.call("cg_rmsprop_update", _p(param), _p(grad), _p(ms), _p(mom), param.numel(), float(lr),
+              float(rho), float(momentum), float(eps), float(grad_scale), _stream(param))
 
 
 # -- bias + activation (lib/graph_conv.py:178-199, fc :220-226) --------------------

@@ -196,6 +196,10 @@ int cg_cheb_backward_ex(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_
  *                    where forward and backward both run the sample-major
  *                    streaming path with Fin a multiple of 16 and K >= 2 (the
  *                    ResGNN hidden layers), else CG_ERR_UNSUPPORTED.
+ *                    x may BE plane 0 (x == basis): a caller whose producer
+ *                    writes the filter input straight into plane 0 (e.g. the
+ *                    previous layer's y) then pays no copy of x -- T_0 is read
+ *                    in place, and the backward reads plane 0 as before.
  * Same values either way (bit-exact basis, y and dx; dW sums its per-wave row
  * chunks in another grouping, so it agrees to fp32 rounding; with the planes
  * layout y sums its inner dimension in another order, agreeing to fp32
@@ -482,6 +486,18 @@ int cg_avgpool_backward(const float* dy, int32_t N, int32_t M, int32_t F, int32_
 int cg_adam_update(float* param, const float* grad, float* m, float* v, int64_t n, float lr,
                    float beta1, float beta2, float eps, int32_t step, float grad_scale,
                    void* stream);
+/* The other update rules gconvRNN.Model._build_optim selects
+ * (lib/gconvRNN.py:381-389: "sgd" / "rmsprop"), as TF 1.x's training ops apply
+ * them, on n fp32 parameters with grad multiplied by grad_scale first:
+ *   cg_sgd_update     (GradientDescentOptimizer): param -= g * lr
+ *   cg_rmsprop_update (RMSPropOptimizer, not centered; TF 1.x defaults rho 0.9,
+ *     momentum 0, eps 1e-10, ms initialised to ONES, mom to zeros):
+ *     ms += (g^2 - ms)(1 - rho); mom = mom*momentum + (g*lr)/sqrt(ms + eps);
+ *     param -= mom */
+int cg_sgd_update(float* param, const float* grad, int64_t n, float lr, float grad_scale,
+                  void* stream);
+int cg_rmsprop_update(float* param, const float* grad, float* ms, float* mom, int64_t n, float lr,
+                      float rho, float momentum, float eps, float grad_scale, void* stream);
 
 /* cg_cheb_backward followed by cg_adam_update(W, dW, m, v, ...) with the
  * optimizer step applied by the dW reduction itself -- for a training step

@@ -58,7 +58,7 @@ def alg_bytes(M, nnz, B, K):
     return (K - 1) * csr + 4 * M * B * (2 + 3 * (K - 2)), (K - 1) * csr + 4 * M * B * (3 + 5 * (K - 2))
 
 
-def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="auto"):
+def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="auto", copy_x=False):
     M = Lt.shape[0]
     plan = ChebPlan(Lt, device=0, variant=variant)
     g = torch.Generator(device=dev)
@@ -71,6 +71,11 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="auto")
     if layout != "rows" and plan.basis_elems(N, Fin, K, Fout, layout) is None:
         return None  # the layout does not apply to this shape
     r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=layout)
+    x_in = "separate buffer (copied into plane 0)" if layout == "planes" else "separate buffer"
+    if layout == "planes" and not copy_x:  # the input lives in plane 0: no copy of x
+        r.input_plane().copy_(x)
+        x = r.input_plane()
+        x_in = "plane 0 of the basis (T_0 read in place)"
     r.forward(x, W)
     r.backward(dy, W)
     torch.cuda.synchronize()
@@ -79,7 +84,7 @@ def filter_config(name, Lt, N, Fin, K, Fout, dev, variant="auto", layout="auto")
     b = ev_ms(lambda: r.backward(dy, W), reps)
     bf, bb = alg_bytes(M, plan.nnz, N * Fin, K)
     return {"config": name, "M": M, "nnz": plan.nnz, "N": N, "Fin": Fin, "K": K, "Fout": Fout,
-            "path": r.path, "variant": variant, "basis_layout": layout,
+            "path": r.path, "variant": variant, "basis_layout": layout, "input": x_in,
             "fwd_ms": round(f, 4), "bwd_ms": round(b, 4),
             "samples_per_s": round(N / ((f + b) * 1e-3), 1),
             "fwd_alg_GBps": round(bf / (f * 1e-3) / 1e9, 1),
@@ -159,6 +164,8 @@ def main():
                     help="basis layout of the C1/C2/D filters (auto: the autograd layers' choice, "
                          "ops.basis_layout_for -- planes where it applies, else rows)")
     ap.add_argument("--rounds", type=int, default=3, help="timed rounds per measurement (median)")
+    ap.add_argument("--copy-x", action="store_true",
+                    help="planes layout: keep x in its own buffer (the forward copies it into plane 0)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -173,7 +180,7 @@ def main():
             with np.load(os.path.join(ROOT, "tests", "golden", "golden_A.npz"), allow_pickle=False) as z:
                 M = int(z["M"])
                 Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
-            out = filter_config("A", Lt, 32, 1, 5, 4, dev, args.variant, args.layout)
+            out = filter_config("A", Lt, 32, 1, 5, 4, dev, args.variant, args.layout, args.copy_x)
             cpu = lambda: bench.cpu_baseline_filter("A", Lt, 32, 32, 1, 5, 4,  # noqa: E731
                                                     seconds=args.cpu_seconds)
         elif name in ("C1", "C2"):
@@ -181,7 +188,7 @@ def main():
                 M = int(z["M"])
                 Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
             Fin = 1 if name == "C1" else 32
-            out = filter_config(name, Lt, 128, Fin, 5, 32, dev, args.variant, args.layout)
+            out = filter_config(name, Lt, 128, Fin, 5, 32, dev, args.variant, args.layout, args.copy_x)
             # the oracle's C2 pass is ~27 s at N = 128: a sub-batch of 8
             nc = 128 if name == "C1" else 8
             cpu = lambda: bench.cpu_baseline_filter(name, Lt, nc, 128, Fin, 5, 32,  # noqa: E731
@@ -190,7 +197,7 @@ def main():
         elif name == "D":
             import synth_graphs
             Lt = rescale_L(synth_graphs.config_d_laplacian(), 2)
-            out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev, args.variant, args.layout)
+            out = filter_config("D", Lt, args.d_batch, 64, 3, 64, dev, args.variant, args.layout, args.copy_x)
             cpu = lambda: bench.cpu_baseline_filter("D", Lt, 1, args.d_batch, 64, 3, 64,  # noqa: E731
                                                     seconds=args.cpu_seconds, warmup=1,
                                                     min_passes=3)

@@ -184,3 +184,10 @@ def test_header_enums_match_the_binding(built_lib):
         assert getattr(_lib, name) == consts[name], name
     assert _lib.BASIS_LAYOUTS == {"rows": consts["CG_BASIS_ROWS"], "orders": consts["CG_BASIS_ORDERS"],
                                   "planes": consts["CG_BASIS_PLANES"]}
+
+
+def test_update_rule_validation(built_lib):
+    h = _lib.lib()
+    assert h.cg_sgd_update(None, None, 4, 0.1, 1.0, None) == _lib.CG_ERR_ARG
+    assert h.cg_sgd_update(None, None, 0, 0.1, 1.0, None) == _lib.CG_ERR_ARG
+    assert h.cg_rmsprop_update(None, None, None, None, 4, 0.1, 0.9, 0.0, 1e-10, 1.0, None) == _lib.CG_ERR_ARG

@@ -311,3 +311,39 @@ def test_planes_layout_skewed_graph(dev):
         T.append(np.stack([2 * (Lt @ T[-1][n]) for n in range(N)]) - T[-2])
     ref = np.stack(T, axis=-1).reshape(N * M, Fin * K)  # column fin*K + k
     assert O.normwise_err(rr.basis.cpu().numpy(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("variant,gname,N,Fin,K,Fout", [("steps", "golden_B.npz", 3, 32, 5, 32),
+                                                        ("auto", "golden_B.npz", 3, 32, 6, 32),
+                                                        ("auto", "golden_C.npz", 2, 32, 5, 32)])
+def test_planes_input_in_plane0_bitwise(dev, variant, gname, N, Fin, K, Fout):
+    """The planes layout with x placed in plane 0 of the basis (x == basis:
+    cg_cheb_forward_layout reads T_0 in place, no copy; the channel-group
+    kernels skip their plane-0 write) against x in its own buffer: basis, y,
+    dx and dW bitwise equal -- on the streaming steps (variant 'steps', and
+    config C's 10 000-vertex graph) and on the channel-group kernels."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    c = case(load_golden(gname))
+    M = c["M"]
+    Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
+    plan = ChebPlan(Lt, device=0, path="stream", variant=variant)
+    rng = np.random.default_rng(N + Fin + K + M)
+    xt = _t(rng.standard_normal((N, M, Fin)), dev)
+    Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
+    dyt = _t(rng.standard_normal((N, M, Fout)), dev)
+    ra = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="planes")
+    rb = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="planes")
+    assert ra.input_plane().data_ptr() == ra.basis.data_ptr()
+    ra.forward(xt, Wt)
+    x0 = rb.input_plane()
+    x0.copy_(xt)
+    rb.forward(x0, Wt)
+    for r in (ra, rb):
+        r.backward(dyt, Wt)
+    torch.cuda.synchronize()
+    assert torch.equal(x0, xt)  # T_0 read in place, never rewritten
+    assert torch.equal(ra.basis, rb.basis)
+    assert torch.equal(ra.y, rb.y)
+    assert torch.equal(ra.dx, rb.dx)
+    assert torch.equal(ra.dW, rb.dW)

@@ -57,3 +57,43 @@ def test_bench_schedule_world2_matches_full_batch(dev, tmp_path):
         assert not np.array_equal(d["W"][n], W0)
         err = O.normwise_err(d["W"][n], full_fused[n].astype(np.float64))
         assert err < 1e-5, (n + 1, err)
+
+
+def _bench_json(args, timeout=400):
+    """Run bench.py as the driver does (no WORLD_SIZE: bench.py starts its own
+    torchrun child) and return its one JSON line."""
+    import json
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(900)
+def test_bench_entry_path_world2(dev):
+    """bench.py's own N > 1 entry: spawn_ranks -> torchrun ->
+    cdist.init -> barrier -> timed steps -> max over ranks -> one JSON line on
+    rank 0, with two ranks sharing this box's GPU over gloo (--dist-backend gloo,
+    test only; RCCL refuses two ranks on one device).  Weak scaling: 256 per GPU,
+    512 in all; strong scaling (--global-batch 256): 128 per GPU."""
+    base = ["--gpus", "2", "--allreduce", "torch", "--dist-backend", "gloo", "--steps", "20",
+            "--warmup", "5"]
+    weak = _bench_json(base)
+    assert weak["n_gpus"] == 2 and weak["steps"] == 20 and weak["warmup"] == 5
+    assert weak["scaling"] == "weak"
+    c = weak["config"]
+    assert c["parallelism"] == "dp2" and c["global_batch"] == 512 and c["batch_per_gpu"] == 256
+    assert c["allreduce"] == "torch" and c["dist_backend"] == "gloo"
+    assert c["adam"].startswith("applied by the next step's forward")
+    assert weak["value"] > 0 and weak["ms_per_step"] > 0
+    assert abs(weak["value"] - 512 * 20 / (weak["ms_per_step"] * 20 / 1e3)) < 0.01 * weak["value"]
+    assert "cpu_baseline" not in weak  # rank 0 at N = 1 only
+    strong = _bench_json(base + ["--global-batch", "256"])
+    assert strong["scaling"] == "strong" and strong["n_gpus"] == 2
+    assert strong["config"]["batch_per_gpu"] == 128 and strong["config"]["global_batch"] == 256
+    assert strong["value"] > 0
