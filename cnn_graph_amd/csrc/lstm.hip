@@ -20,11 +20,12 @@
 // Bytes per row: forward reads 8H (gx, gh) + H (c) and writes 4H (saved
 // activations) + 2H (c', h'); backward reads 4H + 3H (+H dc) and writes 4H + H.
 #include "cg_internal.h"
+#include "lstm_gates.h"
 
 namespace cg {
 namespace {
 
-__device__ __forceinline__ float sigmoidf_(float a) { return 1.f / (1.f + expf(-a)); }
+__device__ __forceinline__ float sigmoidf_(float a) { return gate_sigmoid(a); }
 
 struct GateVals {
   float z, i, f, o;
@@ -33,10 +34,10 @@ struct GateVals {
 template <bool REF>
 __device__ __forceinline__ GateVals activate(float az, float ai, float af, float ao) {
   GateVals g;
-  g.z = REF ? tanf(az) : tanhf(az);
+  g.z = REF ? gate_tan(az) : gate_tanh(az);
   g.i = sigmoidf_(ai);
   g.f = sigmoidf_(af);
-  g.o = REF ? tanhf(ao) : sigmoidf_(ao);
+  g.o = REF ? gate_tanh(ao) : sigmoidf_(ao);
   return g;
 }
 
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(256) void k_lstm_fwd(int total, int H, const float*
     const GateVals g = activate<REF>(az, ai, af, ao);
     const float cp = c ? c[e] : 0.f;
     const float cn = g.f * cp + g.i * g.z;  // ft * c + it * zt (:215)
-    const float hn = g.o * tanhf(cn);       // ot * tanh(new_c) (:218)
+    const float hn = g.o * gate_tanh(cn);   // ot * tanh(new_c) (:218)
     c_out[e] = cn;
     h_out[e] = hn;
     if (act) {
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(int total, int H, const float*
     const int64_t g0 = int64_t(r) * 4 * H + j;
     const float z = act[g0], i = act[g0 + H], f = act[g0 + 2 * H], o = act[g0 + 3 * H];
     const float cp = c ? c[e] : 0.f;
-    const float tc = tanhf(c_out[e]);
+    const float tc = gate_tanh(c_out[e]);
     float dhv = dh ? dh[e] : 0.f;
     if (dh_rec) dhv = dhv + dh_rec[e];
     float dcn = dhv * o * (1.f - tc * tc);

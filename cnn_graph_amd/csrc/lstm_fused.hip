@@ -31,6 +31,7 @@
 // Bound: the fp32 contraction, 2*M*(K*32)*128 FLOP per sample and step, on
 // MFMA (157 TF/s peak) -- with config E's K = 3, 25 MFLOP per sample.
 #include "cg_internal.h"
+#include "lstm_gates.h"
 
 namespace cg {
 namespace {
@@ -42,7 +43,7 @@ constexpr int kQ = 8;      // channels per SpMM pass (quarter of H)
 constexpr int kSR = 12;    // LDS slot row stride (floats)
 constexpr int kWC = 64;    // gate columns per workgroup
 
-__device__ __forceinline__ float sigm(float a) { return 1.f / (1.f + expf(-a)); }
+__device__ __forceinline__ float sigm(float a) { return gate_sigmoid(a); }
 
 struct HStepArgs {
   const int* rowptr;
@@ -221,13 +222,13 @@ __global__ __launch_bounds__(kHT) void k_lstm_hstep(HStepArgs A) {
         af = af + A.bias[64 + j];
         ao = ao + A.bias[96 + j];
       }
-      const float z = A.gates == 0 ? tanf(az) : tanhf(az);
+      const float z = A.gates == 0 ? gate_tan(az) : gate_tanh(az);
       const float ig = sigm(ai), fg = sigm(af);
-      const float o = A.gates == 0 ? tanhf(ao) : sigm(ao);
+      const float o = A.gates == 0 ? gate_tanh(ao) : sigm(ao);
       const float cp = A.c_prev ? A.c_prev[rr * kH + j] : 0.f;
       const float cn = fg * cp + ig * z;
       A.c_out[rr * kH + j] = cn;
-      A.h_out[rr * kH + j] = o * tanhf(cn);
+      A.h_out[rr * kH + j] = o * gate_tanh(cn);
       if (A.act) {
         float* a = A.act + rr * 128 + j;
         a[0] = z;

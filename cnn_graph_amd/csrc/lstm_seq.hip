@@ -52,6 +52,7 @@
 //   over all steps from the forward's planes (one GEMM per order).
 #include "cg_internal.h"
 #include "lds_spmm.h"
+#include "lstm_gates.h"
 
 namespace cg {
 namespace {
@@ -66,7 +67,7 @@ constexpr int kRT = 4;     // forward: 32-row tiles per wave (8 waves x 4 x 32 =
 constexpr int kRB = 8;     // backward: 16-row tiles per wave (8 x 8 x 16 = 1024 rows)
 constexpr int kSeqStaticLds = 64;  // k_lstm_seq's static __shared__ bytes (upper bound)
 
-__device__ __forceinline__ float sigm(float a) { return 1.f / (1.f + expf(-a)); }
+__device__ __forceinline__ float sigm(float a) { return gate_sigmoid(a); }
 
 // agent-scope relaxed accesses: global_load/store ... sc1 (L1 bypass)
 __device__ __forceinline__ float ld_sc1(const float* p) {
@@ -525,7 +526,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           float4 gv[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            gv[g] = (CG_DBG(A.dbg, 16) || A.xs) ? make_float4(0.f, 0.f, 0.f, 0.f)
+            gv[g] = (XPRE || CG_DBG(A.dbg, 16) || A.xs) ? make_float4(0.f, 0.f, 0.f, 0.f)
                                                 : *reinterpret_cast<const float4*>(A.gx + rr * 128 + g * 32 + u0);
           const float4 cv = cva[rt][ct];
           float c[4] = {cv.x, cv.y, cv.z, cv.w};
@@ -552,13 +553,13 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
               c[m] = cn;
               hn[m] = ao * cn;
             } else {
-              z = A.gates == 0 ? tanf(az) : tanhf(az);
+              z = A.gates == 0 ? gate_tan(az) : gate_tanh(az);
               ig = sigm(ai);
               fg = sigm(af);
-              o = A.gates == 0 ? tanhf(ao) : sigm(ao);
+              o = A.gates == 0 ? gate_tanh(ao) : sigm(ao);
               cn = fg * c[m] + ig * z;
               c[m] = cn;
-              hn[m] = o * tanhf(cn);
+              hn[m] = o * gate_tanh(cn);
             }
             zz[m] = z;
             ii[m] = ig;
@@ -705,7 +706,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
       for (int m = 0; m < 8; ++m) {
         // the expressions (and their order) of lstm.hip::k_lstm_bwd
         const float z = av[0][m], i = av[1][m], f = av[2][m], o = av[3][m];
-        const float tc = tanhf(co[m]);
+        const float tc = gate_tanh(co[m]);
         float dh = A.dh ? dhv[m] : 0.f;
         if (A.dh_rec) dh = dh + dhr[m];
         float dcn = dh * o * (1.f - tc * tc);
