@@ -153,7 +153,10 @@ def cpu_baseline(L, fake, K, Fout, n=256, seconds=10.0, warmup=10, min_passes=50
     q = "none" if quota is None else f"{quota:g}"
     return {"value": round(n / med, 1), "unit": "samples/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "pass_ms_median": round(med * 1e3, 2),
+            "pass_ms_p10": round(float(np.percentile(times, 10)) * 1e3, 2),
             "pass_ms_p90": round(float(np.percentile(times, 90)) * 1e3, 2),
+            "value_p10_p90": [round(n / float(np.percentile(times, 90)), 1),
+                              round(n / float(np.percentile(times, 10)), 1)],
             "sample": f"median of {len(times)} timed fwd+bwd passes (after {warmup} warm-up) of the "
                       f"full config-B batch (N={n}, M={M}, K={K}, Fout={Fout}; oracle/cheb_oracle.py, "
                       f"fp32); BLAS threads = {threads} = the CPUs this process may use (affinity "
@@ -178,6 +181,8 @@ def _cpu_leg(name, fn, n, n_full, what, warmup, min_passes, seconds, per_sample=
     sub = "" if n == n_full else f" on a sub-batch of {n} of the config's {n_full} samples per GPU"
     return {"value": round(n / med, 2), "unit": "samples/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "pass_ms_median": round(med * 1e3, 2),
+            "pass_ms_p10": round(float(np.percentile(times, 10)) * 1e3, 2),
+            "pass_ms_p90": round(float(np.percentile(times, 90)) * 1e3, 2),
             "sample": f"config {name}: median of {len(times)} timed fwd+bwd passes{sub}; {what}; BLAS "
                       f"threads = {threads} (affinity {aff}, cgroup quota {q}; os.cpu_count() = {ncpu})"
                       + exc}

@@ -962,7 +962,8 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
                                     dW ? slabs : nullptr, s));
       if (dW) nslab_ready = cg::wide_dypass_blocks(N, M);
       auto G = [&](int k) { return D + size_t(k) * slot; };
-      for (int k = K - 1; k >= 0; --k)
+      // (G_{K-1} = D_{K-1}: the last order's step would rewrite its plane in place)
+      for (int k = K - 2; k >= 0; --k)
         CG_HIP(cg::launch_wide_step(g, plan->trowptr, plan->tcol, plan->tval, plan->trperm,
                                     (k + 1 <= K - 1) ? G(k + 1) : nullptr,
                                     (k + 2 <= K - 1) ? G(k + 2) : nullptr, G(k), G(k), M, B, 2,
@@ -1003,7 +1004,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
         float* D = reinterpret_cast<float*>(rest + al256(size_t(R) * size_t(FinK) * 4));
         CG_HIP(cg::launch_sm_to_vm(dA, K, N, int64_t(M) * Fin, D, s));
         auto G = [&](int k) { return D + size_t(k) * slot; };
-        for (int k = K - 1; k >= 0; --k)
+        for (int k = K - 2; k >= 0; --k)  // (G_{K-1} = D_{K-1} in place: no step)
           CG_HIP(cg::launch_wide_step(g, plan->trowptr, plan->tcol, plan->tval, plan->trperm,
                                       (k + 1 <= K - 1) ? G(k + 1) : nullptr,
                                       (k + 2 <= K - 1) ? G(k + 2) : nullptr, G(k), G(k), M, B, 2,
@@ -1017,7 +1018,10 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       } else {
         const int* rperm = (Fin >= 16) ? plan->trperm : nullptr;
         auto G = [&](int k) { return dA + size_t(k) * slot; };
-        for (int k = K - 1; k >= 0; --k)
+        // G_{K-1} = D_{K-1} already sits in its plane (G lives in place of D):
+        // the last order's step would only rewrite it (D's 17 GB at N = 256);
+        // with K = 1 the one step is dx = D_0
+        for (int k = K >= 2 ? K - 2 : 0; k >= 0; --k)
           CG_HIP(cg::launch_clenshaw(plan->trowptr, plan->tcol, plan->tval, rperm,
                                      (k + 1 <= K - 1) ? G(k + 1) : nullptr,
                                      (k + 2 <= K - 1) ? G(k + 2) : nullptr, k == 0 ? dx : G(k),

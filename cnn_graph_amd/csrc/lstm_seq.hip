@@ -300,7 +300,11 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           }
         }
       };
-      if (XPRE) {
+      // XPRE with feat_in <= 2: the x contraction runs behind the partner's
+      // quarters, its loads issued after the publish drain (issued here they
+      // would wait, one by one, for the previous epilogue's stores)
+      const bool x_late = XPRE && A.Fin <= 2 && K <= 4;
+      if (XPRE && !x_late) {
         // the x basis of step t, precomputed for all steps: MFMA step s takes
         // channel 2s + hh of the lane's rows straight from plane k (L2)
         const int Fin = A.Fin;
@@ -392,15 +396,19 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           // all tiles' loads in flight together; a padding lane (row M) reads
           // past the slab (the descriptor's range check returns 0) and
           // rewrites the zero row with 0
-          float4 v[kRT];
+          // quarter 2u at t > 0: h_{t-1} is already in slot 0 (the previous
+          // epilogue wrote it there: no global load behind its stores)
+          if (!(qq == 0 && t > 0 && (XPRE || !A.xs))) {  // (the fused x recurrence reuses slot 0)
+            float4 v[kRT];
 #pragma unroll
-          for (int rt = 0; rt < kRT; ++rt) {
-            const int off = row[rt] * kH + 8 * q + 4 * hh;
-            v[rt] = (t > 0) ? bld16_sc1(r_hsrc, off) : bld16(r_hsrc, off);
+            for (int rt = 0; rt < kRT; ++rt) {
+              const int off = row[rt] * kH + 8 * q + 4 * hh;
+              v[rt] = (t > 0) ? bld16_sc1(r_hsrc, off) : bld16(r_hsrc, off);
+            }
+#pragma unroll
+            for (int rt = 0; rt < kRT; ++rt)
+              *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = v[rt];
           }
-#pragma unroll
-          for (int rt = 0; rt < kRT; ++rt)
-            *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = v[rt];
           __syncthreads();
           for (int k = 0; k < K; ++k) {
             const float* cur = (k & 1) ? slot1 : slot0;
@@ -496,6 +504,36 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
           contract(2 * (1 - u) + (it + 1) / K, (it + 1) % K, tkb);
         }
       }
+      if (x_late) {
+        // the x basis of step t (channel hh of the lane's rows; a padding row or
+        // a channel past Fin reads past the plane's range: 0), all orders' loads
+        // together
+        const int Fin = A.Fin;
+        float xb[4][kRT];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k >= K) break;
+          const float* xp = A.xplanes + int64_t(k) * A.xpstride + (int64_t(t) * N + n) * M * Fin;
+          const __amdgpu_buffer_rsrc_t rx =
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xp), 0, M * Fin * 4, 0x00020000);
+#pragma unroll
+          for (int rt = 0; rt < kRT; ++rt) {
+            const int xo = (rv[rt] && hh < Fin) ? (row[rt] * Fin + hh) * 4 : M * Fin * 4;
+            xb[k][rt] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, xo, 0, 0));
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (k >= K || CG_DBG(A.dbg, 1)) break;
+          const float* wq = s_Wx + k * 512 + hh * 64 + j;
+          const float a0 = wq[0], a1 = wq[32];
+#pragma unroll
+          for (int rt = 0; rt < kRT; ++rt) {
+            acc[rt][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, xb[k][rt], acc[rt][0], 0, 0, 0);
+            acc[rt][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, xb[k][rt], acc[rt][1], 0, 0, 0);
+          }
+        }
+      }
       if (stamp) CG_TS(A.ts, 3);
       // c_{t-1} of every tile, loaded together before the first store of the
       // epilogue (a load behind stores waits for them: vmcnt counts both):
@@ -571,6 +609,8 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
                 make_float4(c[0], c[1], c[2], c[3]);
           if (!CG_DBG(A.dbg, 256))
             bst16_sc1(r_hout, row[rt] * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
+          if (ct == 0)  // quarter 2u of h_t: the next step's T_0, channels 4hh .. 4hh+3
+            *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = make_float4(hn[0], hn[1], hn[2], hn[3]);
           if (A.act && !CG_DBG(A.dbg, 64)) {
             // unit-major: the 4 gates of a unit side by side, the lane's 4
             // units one contiguous 64-byte record

@@ -164,6 +164,8 @@ def main():
                     help="basis layout of the C1/C2/D filters (auto: the autograd layers' choice, "
                          "ops.basis_layout_for -- planes where it applies, else rows)")
     ap.add_argument("--rounds", type=int, default=3, help="timed rounds per measurement (median)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="kernel-selection option name=value (cg_set_option), e.g. dw_direct=3")
     ap.add_argument("--copy-x", action="store_true",
                     help="planes layout: keep x in its own buffer (the forward copies it into plane 0)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
@@ -173,6 +175,10 @@ def main():
     ROUNDS = args.rounds
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    from cnn_graph_amd import _lib
+    for kv in args.opt:
+        name, val = kv.split("=")
+        _lib.set_option(name, int(val))
     from cnn_graph_amd.graph import rescale_L
     for name in args.configs:
         cpu = None
