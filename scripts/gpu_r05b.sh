@@ -28,3 +28,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktD -o D --output-for
 find $OUT/ktD -name "*kernel_stats.csv" -exec head -8 {} \; | cut -c1-160
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktD3 -o D --output-format csv -- python3 scripts/bench_configs.py D --d-batch 256 --no-cpu --rounds 1 --opt dw_direct=3 > $OUT/ktD3.log 2>&1 || { echo KTD3_FAIL; tail -20 $OUT/ktD3.log; exit 1; }
 find $OUT/ktD3 -name "*kernel_stats.csv" -exec head -8 {} \; | cut -c1-160
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktD4 -o D --output-format csv -- python3 scripts/bench_configs.py D --d-batch 256 --no-cpu --rounds 1 --opt dw_direct=4 > $OUT/ktD4.log 2>&1 || { echo KTD4_FAIL; tail -20 $OUT/ktD4.log; exit 1; }
+find $OUT/ktD4 -name "*kernel_stats.csv" -exec head -8 {} \; | cut -c1-160
+grep config $OUT/ktD4.log
