@@ -112,6 +112,14 @@ __device__ __forceinline__ float4 bld16(__amdgpu_buffer_rsrc_t r, int off) {
   return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
                      __uint_as_float(v.w));
 }
+__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+  u32x4 w;
+  w.x = __float_as_uint(v.x);
+  w.y = __float_as_uint(v.y);
+  w.z = __float_as_uint(v.z);
+  w.w = __float_as_uint(v.w);
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off * 4, 0, 0);
+}
 __device__ __forceinline__ void bst16_sc1(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
   u32x4 w;
   w.x = __float_as_uint(v.x);
@@ -484,14 +492,24 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
         // (sc1 loads, no recurrence here: it computed them)
         // items it = (qq, k), qq-major; item it + 1's loads are in flight
         // during item it's MFMAs (two register sets, alternating)
+        // the row offsets recomputed here from an opaque copy of row[]: offsets
+        // precomputed outside the time loop would be spilled, and each reload
+        // (a vector-memory load, in order with the loads before it) would
+        // serialise these loads one L2 round trip at a time
+        int prow[kRT];
+#pragma unroll
+        for (int rt = 0; rt < kRT; ++rt) {
+          prow[rt] = row[rt] * kH + 4 * hh;
+          asm volatile("" : "+v"(prow[rt]));
+        }
         auto ldq = [&](int it, float4 (&tk)[kRT]) {
           const int q = 2 * (1 - u) + it / K, k = it % K;
           const float* src = (k == 0) ? hsrc : pl_t + int64_t(k - 1) * A.pstride;
           const __amdgpu_buffer_rsrc_t r_src = slab_rsrc(src, M);
 #pragma unroll
           for (int rt = 0; rt < kRT; ++rt) {  // row M: past the slab, reads 0
-            const int off = row[rt] * kH + 8 * q + 4 * hh;
-            tk[rt] = (k == 0 && t == 0) ? bld16(r_src, off) : bld16_sc1(r_src, off);
+            const int off = prow[rt] + 8 * q;
+            tk[rt] = bld16_sc1(r_src, off);  // (h0 too: one form, no branch per load)
           }
         };
         const int nit = 2 * K;
@@ -554,12 +572,21 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
       }
       // gate update: lane (row, hh) of tile (rt, ct) holds gates g = 0..3 of
       // units 16u + 8ct + 4hh + m in acc[rt][ct][4g + m]
+      // (c and act leave through buffer stores over the step's slabs: 32-bit
+      // offsets from the row instead of a 64-bit address per tile)
+      const int64_t slab0 = (int64_t(t) * N + n) * M;
+      const __amdgpu_buffer_rsrc_t r_cout = slab_rsrc(A.cs + slab0 * kH, M);
+      const __amdgpu_buffer_rsrc_t r_act = __builtin_amdgcn_make_buffer_rsrc(
+          A.act ? A.act + slab0 * 128 : A.cs, 0, A.act && !CG_DBG(A.dbg, 64) ? M * 512 : 0, 0x00020000);
 #pragma unroll
       for (int rt = 0; rt < kRT; ++rt) {
         if (!rv[rt]) continue;
-        const int64_t rr = (int64_t(t) * N + n) * M + row[rt];
+        const int64_t rr = slab0 + row[rt];
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
+          // one tile's gate math at a time (interleaving tiles costs registers
+          // the kernel does not have: spills, whose reloads wait for the stores)
+          __builtin_amdgcn_sched_barrier(0);
           const int u0 = 16 * u + 8 * ct + 4 * hh;
           float4 gv[4];
 #pragma unroll
@@ -604,21 +631,16 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
             ff[m] = fg;
             oo[m] = o;
           }
-          if (!CG_DBG(A.dbg, 128))
-            *reinterpret_cast<float4*>(A.cs + rr * kH + u0) =
-                make_float4(c[0], c[1], c[2], c[3]);
+          if (!CG_DBG(A.dbg, 128)) bst16(r_cout, row[rt] * kH + u0, make_float4(c[0], c[1], c[2], c[3]));
           if (!CG_DBG(A.dbg, 256))
             bst16_sc1(r_hout, row[rt] * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
           if (ct == 0)  // quarter 2u of h_t: the next step's T_0, channels 4hh .. 4hh+3
             *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = make_float4(hn[0], hn[1], hn[2], hn[3]);
-          if (A.act && !CG_DBG(A.dbg, 64)) {
-            // unit-major: the 4 gates of a unit side by side, the lane's 4
-            // units one contiguous 64-byte record
-            float* ap = A.act + rr * 128 + 4 * u0;
+          // unit-major act: the 4 gates of a unit side by side, the lane's 4
+          // units one contiguous 64-byte record (no act: a 0-byte range)
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
-              *reinterpret_cast<float4*>(ap + 4 * m) = make_float4(zz[m], ii[m], ff[m], oo[m]);
-          }
+          for (int m = 0; m < 4; ++m)
+            bst16(r_act, row[rt] * 128 + 4 * u0 + 4 * m, make_float4(zz[m], ii[m], ff[m], oo[m]));
         }
       }
       if (stamp) CG_TS(A.ts, 4);
