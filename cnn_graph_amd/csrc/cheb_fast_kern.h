@@ -225,71 +225,49 @@ struct Fwd {
     gB = a.basis ? a.basis + size_t(blockIdx.x) * FinK * bord : nullptr;
   }
 
-  // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA, split over the two
-  // steps that follow it: pair_load(s) (once T_{2s+1} is complete) reads the
-  // lane's operands of both its tiles from the ring -- and stages the basis
-  // (rows layout) or stores it (orders layout: a half-wave's 32 rows of one
+  // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA; stage the basis
+  // (rows layout) or store it (orders layout: a half-wave's 32 rows of one
   // order are 128 contiguous bytes, so each store is two whole lines and the
-  // basis leaves during the recurrence instead of after it) -- and each of
-  // the two steps issues ONE tile's MFMAs right behind its gathers.  With both
-  // tiles' MFMAs issued together after a barrier, the 4 waves of a SIMD queue
-  // 8 MFMAs on its one matrix pipe and the last wave waits ~450 cycles to
-  // reach its gathers (the ~2.3 us of pipe time the round-2 ablation found
-  // unhidden); one MFMA per wave per step sits in the shadow of the gathers.
-  float pa[MT][FV];  // A operands of the pending pair (per tile, per fin)
-  float pb[FV][NT];  // its B operands (W rows of the two orders, per lane half)
-
-  __device__ __forceinline__ void pair_load(int s) {
+  // basis leaves during the recurrence instead of after it).
+  __device__ __forceinline__ void pair(int s) {
     const int kk = 2 * s + h;
     const bool kv = kk < K;
     const int soff = (kk % 3) * 4 * FV;
 #pragma unroll
     for (int fin = 0; fin < FV; ++fin) {
+      float b[NT];
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
         const int f = q * 32 + li;
-        pb[fin][q] = (kv && f < Fout) ? s_W[(fin * K + kk) * Fout + f] : 0.f;
+        b[q] = (kv && f < Fout) ? s_W[(fin * K + kk) * Fout + f] : 0.f;
       }
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const int tile = wave + t * kW;
-        float a = 0.f;
-        if (kv && tile < ntiles) {
+        if (tile < ntiles) {
           const int m = tile * 32 + li;
-          a = lds_f(ring + mb[t] + soff + fin * 4);
-          if (keep_basis) {
-            if (OB) gB[(fin * K + kk) * bord + m] = a;  // rows >= M: the zero record
-            else if (m < M) s_B[m * FinK + fin * K + kk] = a;
+          float a = 0.f;
+          if (kv) {
+            a = lds_f(ring + mb[t] + soff + fin * 4);
+            if (keep_basis) {
+              if (OB) gB[(fin * K + kk) * bord + m] = a;  // rows >= M: the zero record
+              else if (m < M) s_B[m * FinK + fin * K + kk] = a;
+            }
+          }
+          if (!CG_DBG(A.dbg, 4)) {
+#pragma unroll
+            for (int q = 0; q < NT; ++q) acc[t][q] = mfma32(a, b[q], acc[t][q]);
           }
         }
-        pa[t][fin] = a;
       }
     }
   }
 
-  __device__ __forceinline__ void pair_mma(int t) {
-    if (CG_DBG(A.dbg, 4) || wave + t * kW >= ntiles) return;
-#pragma unroll
-    for (int fin = 0; fin < FV; ++fin)
-#pragma unroll
-      for (int q = 0; q < NT; ++q) acc[t][q] = mfma32(pa[t][fin], pb[fin][q], acc[t][q]);
-  }
-
-  // step k; mt >= 0: tile mt's MFMAs of the pending pair, behind the gathers
   template <int L, int CUR, int PRV, int PRV2>
-  __device__ __forceinline__ void step(int k, int mt) {
+  __device__ __forceinline__ void step(int k) {
 #pragma clang fp contract(off)
     // ablation build: 64 skips the gathers, 128 the own-record writes (LDS attribution)
-    V a;
-    if (CG_DBG(A.dbg, 64)) {
-      a = r.v[0] * t1;
-      if (mt >= 0) pair_mma(mt);
-    } else {
-      V g[L > 0 ? L : 1];
-      r.template gather<FV, L, PRV>(ring, g);
-      if (mt >= 0) pair_mma(mt);
-      a = r.template reduce<FV, L>(g);
-    }
+    const V a = CG_DBG(A.dbg, 64) ? r.v[0] * t1 : r.template dot<FV, L, PRV>(ring);
     V o;
     if (CG_DBG(A.dbg, 32)) {  // A/B switch: T_{k-2} of the own row re-read from the ring
       const V p = lds_v<FV>(ring + r.rr + PRV2 * 4 * FV);
@@ -361,24 +339,17 @@ struct Fwd {
     run<L>();
   }
 
-  // pair s is loaded before step 2s + 2 (T_{2s+1} complete; its ring slots are
-  // overwritten from step 2s + 3 on, after that step's barrier), its tile 0 is
-  // contracted in step 2s + 2 and its tile 1 in step 2s + 3; the last pair
-  // (and a tile 1 with no step left) after the recurrence
   template <int L>
   __device__ __forceinline__ void run() {
     for (int k = 1; k < K; k += 6) {  // k = 1 (mod 6): slots cur/prv/prv2 = 1/0/2
-      step<L, 1, 0, 2>(k, k >= 3 ? 1 : -1);
-      if (k + 1 < K) { pair_load((k - 1) >> 1); step<L, 2, 1, 0>(k + 1, 0); }
-      if (k + 2 < K) step<L, 0, 2, 1>(k + 2, 1);
-      if (k + 3 < K) { pair_load((k + 1) >> 1); step<L, 1, 0, 2>(k + 3, 0); }
-      if (k + 4 < K) step<L, 2, 1, 0>(k + 4, 1);
-      if (k + 5 < K) { pair_load((k + 3) >> 1); step<L, 0, 2, 1>(k + 5, 0); }
+      step<L, 1, 0, 2>(k);
+      if (k + 1 < K) { pair((k - 1) >> 1); step<L, 2, 1, 0>(k + 1); }
+      if (k + 2 < K) step<L, 0, 2, 1>(k + 2);
+      if (k + 3 < K) { pair((k + 1) >> 1); step<L, 1, 0, 2>(k + 3); }
+      if (k + 4 < K) step<L, 2, 1, 0>(k + 4);
+      if (k + 5 < K) { pair((k + 3) >> 1); step<L, 0, 2, 1>(k + 5); }
     }
-    if (K >= 3 && (K & 1)) pair_mma(1);  // tile 1 of pair (K - 3) / 2: step K does not exist
-    pair_load((K - 1) >> 1);  // the last (possibly half-empty) pair
-    pair_mma(0);
-    pair_mma(1);
+    pair((K - 1) >> 1);  // the last (possibly half-empty) pair
   }
 };
 

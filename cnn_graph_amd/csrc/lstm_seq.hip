@@ -312,7 +312,9 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
       // quarters, its loads issued after the publish drain (issued here they
       // would wait, one by one, for the previous epilogue's stores)
       const bool x_late = XPRE && A.Fin <= 2 && K <= 4;
-      if (XPRE && !x_late) {
+      if (XPRE && x_late) {
+        // contracted behind the partner's quarters (below)
+      } else if (XPRE) {
         // the x basis of step t, precomputed for all steps: MFMA step s takes
         // channel 2s + hh of the lane's rows straight from plane k (L2)
         const int Fin = A.Fin;

@@ -11,17 +11,6 @@ timeout -k 10 300 python scripts/bench_configs.py E E C1 C2 D --d-batch 256 --no
 grep config $OUT/cfg.jsonl
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktE -o E --output-format csv -- python3 scripts/bench_configs.py E --no-cpu > $OUT/ktE.log 2>&1 || { echo KT_FAIL; tail -20 $OUT/ktE.log; exit 1; }
 find $OUT/ktE -name "*kernel_stats.csv" -exec head -4 {} \; | cut -c1-160
-for i in 1 2; do
-  timeout -k 10 300 python bench.py --steps 400 --warmup 40 --no-cpu-baseline > $OUT/bench_new$i.json 2>&1 || { echo BENCH_FAIL; tail -20 $OUT/bench_new$i.json; exit 1; }
-  CG_LIB_PATH=scripts/ablib/libcheb_base.so timeout -k 10 300 python bench.py --steps 400 --warmup 40 --no-cpu-baseline > $OUT/bench_base$i.json 2>&1 || { echo BENCHB_FAIL; tail -20 $OUT/bench_base$i.json; exit 1; }
-done
-python3 - <<'PY'
-import json,glob,os
-out=os.environ.get('OUT','')
-for f in sorted(glob.glob('gpurun_out/r05b/bench_*.json')):
-    d=json.loads(open(f).read().strip().splitlines()[-1])
-    print(f.split('/')[-1], d['value'], d['ms_per_step'], d['kernels']['fwd']['avg_ms'], d['kernels']['bwd']['avg_ms'])
-PY
 timeout -k 10 300 python scripts/bench_configs.py D --d-batch 256 --no-cpu --opt dw_direct=3 > $OUT/D_dw3.jsonl 2>&1 || { echo D3_FAIL; tail -20 $OUT/D_dw3.jsonl; exit 1; }
 grep config $OUT/D_dw3.jsonl
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktD -o D --output-format csv -- python3 scripts/bench_configs.py D --d-batch 256 --no-cpu --rounds 1 > $OUT/ktD.log 2>&1 || { echo KTD_FAIL; tail -20 $OUT/ktD.log; exit 1; }
