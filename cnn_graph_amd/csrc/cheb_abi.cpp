@@ -460,7 +460,7 @@ namespace {
 std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}};
 bool option_valid(int o, int v) {
   switch (o) {
-    case kOptDwDirect: return v >= 0 && v <= 4;
+    case kOptDwDirect: return v >= 0 && v <= 3;
     case kOptDwWaves: return v == 4 || v == 8;
     case kOptClenDy: return v >= 0 && v <= 2;
     default: return v == 0 || v == 1;

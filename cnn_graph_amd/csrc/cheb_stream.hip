@@ -1129,9 +1129,9 @@ static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int
     // two-float basis loads, six virtual tiles: FinK <= 192 in ONE column
     // group, so dy is read once (config D: 17.5 ms per call against 19.7 for
     // <1, 3, ...> and 20.6 for k_dw_slabs, profiles/r04_d)
-    // CG_OPT_DW_DIRECT = 4: two-float loads in three groups of two virtual
-    // tiles (4 tiles, 64 accumulators): two waves per SIMD (A/B)
-    if (a2 && mode == 4) return go(k_dw_direct2<2, 1, 2, 1, 12>, 2);
+    // (two waves per SIMD measured slower on config D at N = 256, 19.8 ms per
+    // call for both <1, 3, 2, 1, 12> and two-float <2, 1, 2, 1, 12> in three
+    // groups of two tiles: profiles/r05_b)
     if (a2 && mode != 3) return go(k_dw_direct<2, 3, 2, 1, 8>, 6);
     return w2 ? go(k_dw_direct2<1, 3, 2, 1, 12>, 3) : go(k_dw_direct<1, 3, 2, 1, 12>, 3);
   }

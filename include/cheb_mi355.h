@@ -73,9 +73,7 @@ enum {
 enum {
   CG_OPT_DW_DIRECT = 0, /* 1: k_dw_direct where a chunk has >= 256 rows and the grid fills
                            the chip (default); 0: k_dw_slabs; 2: k_dw_direct whatever the
-                           wave count; 3: as 2 with one-float basis loads only; 4: as 2
-                           with two-float loads in groups of two tiles, two waves per
-                           SIMD (Fout <= 64)                                           */
+                           wave count; 3: as 2 with one-float basis loads only        */
   CG_OPT_DW_W2 = 1,     /* 1: the two-waves-per-SIMD build of k_dw_direct where it fits
                            (default); 0: the one-wave build                           */
   CG_OPT_DW_WAVES = 2,  /* waves per k_dw_slabs block: 8 (default) or 4               */
