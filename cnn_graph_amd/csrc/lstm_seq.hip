@@ -185,7 +185,9 @@ __device__ void lstm_seq_poison(const SeqArgs& A, int n0, int t0, int u) {
     }
 }
 
-template <bool XPRE>
+// REF: the reference gate set (z = tan, o = tanh), a template parameter so the
+// epilogue carries one gate set, not both behind selects
+template <bool XPRE, bool REF>
 __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -209,6 +211,11 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
   float* s_b = s_Wx + (A.xs ? K * 512 : 0);  // [128] bias (zeros when NULL)
   float* s_val = s_b + 128;
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
+  // the lanes' rows, [rt][tid]: the epilogue reads its store offsets from here
+  // (an LDS read waits for no store; a spilled offset's scratch reload waits
+  // for every store before it -- the write-through h store above all)
+  int* s_rowt = reinterpret_cast<int*>(reinterpret_cast<char*>(s_col) +
+                                       align16(size_t(A.nnz) * 2 + kSpmmSlack));
   // A operands of the transposed contraction: lane (i, hh) of MFMA step s in
   // quarter q, order k holds Wh[(8q + 4hh + s) K + k][gate column of tile
   // row i] -- tile ct's rows i = 8 g + m are gate g, unit 16u + 8ct + m
@@ -254,6 +261,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
     rb[rt] = rvS[rt] ? A.rowptr[rowS[rt]] : 0;
     re[rt] = rvS[rt] ? A.rowptr[rowS[rt] + 1] : 0;
     wl[rt] = wave_max(re[rt] - rb[rt]);  // the tile's longest row: its unrolled gather count
+    s_rowt[rt * kST + tid] = row[rt];
   }
   __syncthreads();
 
@@ -583,13 +591,17 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
 #pragma unroll
       for (int rt = 0; rt < kRT; ++rt) {
         if (!rv[rt]) continue;
-        const int64_t rr = slab0 + row[rt];
+        int erow = s_rowt[rt * kST + tid];  // == row[rt]
+        asm volatile("" : "+v"(erow));
+        const int64_t rr = slab0 + erow;
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
           // one tile's gate math at a time (interleaving tiles costs registers
           // the kernel does not have: spills, whose reloads wait for the stores)
           __builtin_amdgcn_sched_barrier(0);
-          const int u0 = 16 * u + 8 * ct + 4 * hh;
+          int lq = threadIdx.x;  // 4hh re-derived per tile (a hoisted copy would spill)
+          asm volatile("" : "+v"(lq));
+          const int u0 = 16 * u + 8 * ct + ((lq >> 3) & 4);
           float4 gv[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g)
@@ -620,10 +632,10 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
               c[m] = cn;
               hn[m] = ao * cn;
             } else {
-              z = A.gates == 0 ? gate_tan(az) : gate_tanh(az);
+              z = REF ? gate_tan(az) : gate_tanh(az);
               ig = sigm(ai);
               fg = sigm(af);
-              o = A.gates == 0 ? gate_tanh(ao) : sigm(ao);
+              o = REF ? gate_tanh(ao) : sigm(ao);
               cn = fg * c[m] + ig * z;
               c[m] = cn;
               hn[m] = o * gate_tanh(cn);
@@ -633,16 +645,41 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
             ff[m] = fg;
             oo[m] = o;
           }
-          if (!CG_DBG(A.dbg, 128)) bst16(r_cout, row[rt] * kH + u0, make_float4(c[0], c[1], c[2], c[3]));
-          if (!CG_DBG(A.dbg, 256))
-            bst16_sc1(r_hout, row[rt] * kH + u0, make_float4(hn[0], hn[1], hn[2], hn[3]));
-          if (ct == 0)  // quarter 2u of h_t: the next step's T_0, channels 4hh .. 4hh+3
-            *reinterpret_cast<float4*>(slot0 + row[rt] * kQ + 4 * hh) = make_float4(hn[0], hn[1], hn[2], hn[3]);
+          // the tile's store offsets, formed here from the LDS row (laundered:
+          // hoisted lane constants would spill, and their reloads wait for stores)
+          int ec = erow * kH + u0, ea = erow * 128 + 4 * u0;
+          asm volatile("" : "+v"(ec), "+v"(ea));
+          if (!CG_DBG(A.dbg, 128)) bst16(r_cout, ec, make_float4(c[0], c[1], c[2], c[3]));
+          // h_t of quarter 2u + ct into its slot (channels 4hh .. 4hh+3): quarter
+          // 2u is the next step's T_0; both leave write-through after the tiles
+          int es = erow * kQ + (ct == 0 ? 0 : A.Mr * kQ) + ((lq >> 3) & 4);  // slot0 / slot1
+          asm volatile("" : "+v"(es));
+          *reinterpret_cast<float4*>(smem + es) = make_float4(hn[0], hn[1], hn[2], hn[3]);
           // unit-major act: the 4 gates of a unit side by side, the lane's 4
           // units one contiguous 64-byte record (no act: a 0-byte range)
 #pragma unroll
           for (int m = 0; m < 4; ++m)
-            bst16(r_act, row[rt] * 128 + 4 * u0 + 4 * m, make_float4(zz[m], ii[m], ff[m], oo[m]));
+            bst16(r_act, ea + 4 * m, make_float4(zz[m], ii[m], ff[m], oo[m]));
+        }
+      }
+      // h_t of the lane's own slots (its own writes above), write-through: the
+      // last vector-memory ops of the step, so no load of this step waits for
+      // them (the next publish drains them, a quarter recurrence later)
+      if (!CG_DBG(A.dbg, 256)) {
+#pragma unroll
+        for (int rt = 0; rt < kRT; ++rt) {
+          if (!rv[rt]) continue;
+          int erow = s_rowt[rt * kST + tid];
+          asm volatile("" : "+v"(erow));
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) {
+            int lq = threadIdx.x;
+            asm volatile("" : "+v"(lq));
+            const int h4 = (lq >> 3) & 4;  // 4hh
+            const int eh = erow * kH + 16 * u + 8 * ct + h4;
+            const int es = erow * kQ + (ct == 0 ? 0 : A.Mr * kQ) + h4;
+            bst16_sc1(r_hout, eh, *reinterpret_cast<const float4*>(smem + es));
+          }
         }
       }
       if (stamp) CG_TS(A.ts, 4);
@@ -889,7 +926,7 @@ inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
 size_t lstm_seq_lds(int M, int K, int64_t nnz, int xfin) {
   return size_t(2) * round_up(M + 1, 32) * kQ * 4 + size_t(K) * 2048 * 4 +
          (xfin > 0 ? size_t(K) * 512 * 4 : 0) + 512 + size_t(nnz) * 4 +
-         align16(size_t(nnz) * 2 + kSpmmSlack);
+         align16(size_t(nnz) * 2 + kSpmmSlack) + size_t(kRT) * kST * 4;  // + the lanes' row table
 }
 
 bool lstm_seq_ok(int M, int H, int K, int64_t nnz, int xfin) {
@@ -926,14 +963,20 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
       (xs && (Fin < 1 || Fin > 8 || !Wx || !xplanes)) || (!xs && !gx))
     return hipErrorInvalidValue;
   // the kernel's static LDS (the abort word) counts against the same 160 KB
-  static hipError_t attr0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_seq<false>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                kLdsBytes - kSeqStaticLds);
-  static hipError_t attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_seq<true>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                kLdsBytes - kSeqStaticLds);
-  if (attr0 != hipSuccess) return attr0;
-  if (attr1 != hipSuccess) return attr1;
+  // [xpre][reference gates]
+  static void (*const kerns[2][2])(SeqArgs) = {{&k_lstm_seq<false, false>, &k_lstm_seq<false, true>},
+                                               {&k_lstm_seq<true, false>, &k_lstm_seq<true, true>}};
+  static const hipError_t attr = [] {
+    for (auto& row : kerns)
+      for (auto* k : row) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 kLdsBytes - kSeqStaticLds);
+        if (e != hipSuccess) return e;
+      }
+    return hipSuccess;
+  }();
+  if (attr != hipSuccess) return attr;
   int dev = 0, rate_khz = 0;
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
@@ -942,7 +985,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   SeqArgs a{rowptr, col, val, order, M, round_up(M + 1, 32), K, N, T, gates, int(nnz), P,
             P % 8 == 0 ? 1 : 0, gx, xs, Wx, xplanes, xpstride, Fin, Wh, bias, h0, c0, hs, cs, act, planes, pstride, flags, status,
             // a pair hand-off that has not happened after 2 s ends the launch
-            static_cast<unsigned long long>(rate_khz) * 2000ull, (debug_flags() >> 16) & 0xff,
+            static_cast<unsigned long long>(rate_khz) * 2000ull, (debug_flags() >> 16) & 0x1ff,
             nullptr, 0, inject_t};
 #ifdef CG_DEBUG
   a.ts = g_debug_ts;
@@ -974,8 +1017,8 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   // other streams or processes can hold CUs, which is what the hand-off
   // timeout, the NaN poisoning and the plan's fault word are for
   const size_t lds = lstm_seq_lds(M, K, nnz, xs ? Fin : 0);
-  const void* kern = a.xpre ? reinterpret_cast<const void*>(&k_lstm_seq<true>)
-                            : reinterpret_cast<const void*>(&k_lstm_seq<false>);
+  void (*const kfn)(SeqArgs) = kerns[a.xpre ? 1 : 0][gates == 0 ? 1 : 0];
+  const void* kern = reinterpret_cast<const void*>(kfn);
   int per_cu = 0, cus = 0;
   e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kST, lds);
   if (e != hipSuccess) return e;
@@ -983,8 +1026,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   if (e != hipSuccess) return e;
   if (per_cu < 1 || 2 * P > per_cu * cus) return hipErrorCooperativeLaunchTooLarge;
   const dim3 grid(2 * P), block(kST);
-  if (a.xpre) hipLaunchKernelGGL(k_lstm_seq<true>, grid, block, lds, s, a);
-  else hipLaunchKernelGGL(k_lstm_seq<false>, grid, block, lds, s, a);
+  hipLaunchKernelGGL(kfn, grid, block, lds, s, a);
   return hipGetLastError();
 }
 
