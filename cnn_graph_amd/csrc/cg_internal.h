@@ -74,6 +74,32 @@ __device__ __forceinline__ void stage_lds(int n, LD&& ld, ST&& st) {
   }
 }
 
+// CSR values and 16-bit columns into LDS, U loads of each in flight per thread
+// (one load per iteration leaves every iteration a full memory latency)
+template <int U, int NT>
+__device__ __forceinline__ void stage_csr_lds(int nnz, const float* __restrict__ val,
+                                              const int* __restrict__ col, float* s_val,
+                                              unsigned short* s_col) {
+  for (int e0 = int(threadIdx.x); e0 < nnz; e0 += U * NT) {
+    float v[U];
+    int c[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e = e0 + q * NT;
+      v[q] = e < nnz ? val[e] : 0.f;
+      c[q] = e < nnz ? col[e] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int e = e0 + q * NT;
+      if (e < nnz) {
+        s_val[e] = v[q];
+        s_col[e] = static_cast<unsigned short>(c[q]);
+      }
+    }
+  }
+}
+
 // ---- resident (LDS) path ---------------------------------------------------
 struct ResidentGeom {
   int nnz;         // nonzeros of L~ (== of L~^T); the resident path needs nnz >= 1
@@ -370,7 +396,7 @@ hipError_t launch_lstm_fwd(int gates, int64_t R, int H, const float* gx, const f
 hipError_t launch_lstm_bwd(int gates, int64_t R, int H, const float* dh, const float* dh_rec,
                            const float* dc,
                            const float* act, const float* c, const float* c_out, float* dpre,
-                           float* dc_prev, hipStream_t s);
+                           float* dc_prev, hipStream_t s, int act_um = 0);
 // One time step's h path of the gconv-LSTM in one launch (lstm_fused.hip):
 // the Chebyshev basis of h_prev in LDS, gh = basis Wh on MFMA, the gate
 // update; planes (nullable) receive T_1..T_{K-1} of h_prev ([N][M][H] each,

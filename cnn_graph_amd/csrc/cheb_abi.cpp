@@ -1741,8 +1741,8 @@ int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gat
   int rc = check_lstm(int64_t(N) * (plan ? plan->M : 1), H, gates);
   if (rc) return rc;
   if (!plan || N < 1 || K < 1) return fail(CG_ERR_ARG, "lstm_bwd_step: bad plan / N / K");
-  if (!act || !c_out || !Wh || !dpre || !dh_prev)
-    return fail(CG_ERR_ARG, "lstm_bwd_step: null act / c_out / Wh / dpre / dh_prev");
+  if (!act || !c_out || !Wh || !dpre)
+    return fail(CG_ERR_ARG, "lstm_bwd_step: null act / c_out / Wh / dpre");
   if (!cg::lstm_bstep_ok(plan->M, H, K, plan->nnzT))
     return fail(CG_ERR_UNSUPPORTED, "lstm_bwd_step: needs H = 32, M <= 1024, K <= 4 (M=%d H=%d K=%d)",
                 plan->M, H, K);
@@ -1755,6 +1755,12 @@ int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gat
     for (const void* i : ins)
       if (o && o == i) return fail(CG_ERR_ARG, "lstm_bwd_step: outputs must not alias inputs");
   if ((rc = check_device(plan))) return rc;
+  if (!dh_prev) {  // no h-conv at this step (a zero-state layer's step 0): the pointwise part
+    CG_HIP(cg::launch_lstm_bwd(gates, int64_t(N) * plan->M, H, dh, dh_rec, dc, act, c_prev, c_out,
+                               dpre, dc_prev, reinterpret_cast<hipStream_t>(stream),
+                               act_unit_major));
+    return ok();
+  }
   CG_HIP(cg::launch_lstm_bstep(gates, N, plan->M, K, plan->trowptr, plan->tcol, plan->tval,
                                plan->tlorder, plan->nnzT, dh, dh_rec,
                                dc, act, act_unit_major, c_prev, c_out, Wh, dpre, dc_prev, dh_prev,

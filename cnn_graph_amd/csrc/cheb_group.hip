@@ -95,10 +95,7 @@ __global__ __launch_bounds__(kGT) void k_grp_fwd(GrpFwdArgs A) {
       return out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
     }, [&](int e, float v) { s_W[e] = v; });
   }
-  for (int e = tid; e < A.nnz; e += kGT) {
-    s_val[e] = A.val[e];
-    s_col[e] = static_cast<unsigned short>(A.col[e]);
-  }
+  stage_csr_lds<8, kGT>(A.nnz, A.val, A.col, s_val, s_col);
   if (tid < 2 * kGQ) (tid < kGQ ? slot0 : slot1)[M * kGQ + (tid & (kGQ - 1))] = 0.f;  // zero row M
   // two lane mappings over the same 32 rows of tile (wave, rt): the MFMA's
   // (row j = lane % 32, half hh = lane / 32) reads its B operand from the slot;
@@ -237,10 +234,7 @@ __global__ __launch_bounds__(kGT) void k_grp16_fwd(GrpFwdArgs A) {
       return out < Fout ? A.W[int64_t(ch * K + k) * Fout + out] : 0.f;
     }, [&](int e, float v) { s_W[e] = v; });
   }
-  for (int e = tid; e < A.nnz; e += kGT) {
-    s_val[e] = A.val[e];
-    s_col[e] = static_cast<unsigned short>(A.col[e]);
-  }
+  stage_csr_lds<8, kGT>(A.nnz, A.val, A.col, s_val, s_col);
   if (tid < kGQ16) slot[M * kGQ16 + tid] = 0.f;  // zero row M
   const int js = lane >> 2, qs = lane & 3;
   const int c0 = kGQ16 * g + 4 * qs;
@@ -440,10 +434,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen(GrpClenArgs A) {
   float* slotB = smem + A.Mr * kGQ;
   float* s_val = slotB + A.Mr * kGQ;
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
-  for (int e = tid; e < A.nnz; e += kGT) {
-    s_val[e] = A.tval[e];
-    s_col[e] = static_cast<unsigned short>(A.tcol[e]);
-  }
+  stage_csr_lds<8, kGT>(A.nnz, A.tval, A.tcol, s_val, s_col);
   int row[kGRT], rb[kGRT], re[kGRT], wl[kGRT];
   bool rv[kGRT];
   int64_t off[kGRT];
@@ -605,10 +596,7 @@ __global__ __launch_bounds__(kGT) void k_grp_clen_dy(GrpClenDyArgs A) {
   float* s_val = s_w + K * kGQ * WS;
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
   const int c0 = kGQ * g;
-  for (int e = tid; e < A.nnz; e += kGT) {
-    s_val[e] = A.tval[e];
-    s_col[e] = static_cast<unsigned short>(A.tcol[e]);
-  }
+  stage_csr_lds<8, kGT>(A.nnz, A.tval, A.tcol, s_val, s_col);
   stage_lds<8, kGT>(K * kGQ * Fout, [&](int e) {
     const int f = e % Fout, kc = e / Fout, ch = kc % kGQ, k = kc / kGQ;
     return A.W[(int64_t(c0 + ch) * K + k) * Fout + f];

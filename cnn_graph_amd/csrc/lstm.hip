@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_lstm_fwd(int total, int H, const float*
 // the pre-activation gradients dpre [R][4H] (the dy of the x- and h-conv
 // contractions and of the bias) and dc_prev = dL/dc.
 template <bool REF>
-__global__ __launch_bounds__(256) void k_lstm_bwd(int total, int H, const float* __restrict__ dh,
+__global__ __launch_bounds__(256) void k_lstm_bwd(int total, int H, int act_um, const float* __restrict__ dh,
                                                   const float* __restrict__ dh_rec,
                                                   const float* __restrict__ dc,
                                                   const float* __restrict__ act,
@@ -101,7 +101,10 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(int total, int H, const float*
   for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
     const int r = e / H, j = e - r * H;
     const int64_t g0 = int64_t(r) * 4 * H + j;
-    const float z = act[g0], i = act[g0 + H], f = act[g0 + 2 * H], o = act[g0 + 3 * H];
+    // act gate-major [R][4][H] or unit-major [R][H][4] (the sequence kernel's records)
+    const int64_t a0 = act_um ? int64_t(r) * 4 * H + 4 * j : g0;
+    const int as = act_um ? 1 : H;
+    const float z = act[a0], i = act[a0 + as], f = act[a0 + 2 * as], o = act[a0 + 3 * as];
     const float cp = c ? c[e] : 0.f;
     const float tc = gate_tanh(c_out[e]);
     float dhv = dh ? dh[e] : 0.f;
@@ -165,14 +168,14 @@ hipError_t launch_lstm_fwd(int gates, int64_t R, int H, const float* gx, const f
 hipError_t launch_lstm_bwd(int gates, int64_t R, int H, const float* dh, const float* dh_rec,
                            const float* dc,
                            const float* act, const float* c, const float* c_out, float* dpre,
-                           float* dc_prev, hipStream_t s) {
+                           float* dc_prev, hipStream_t s, int act_um) {
   const int total = int(R * H);
   if (gates == 0)
-    hipLaunchKernelGGL(k_lstm_bwd<true>, dim3(grid1d(total)), dim3(256), 0, s, total, H, dh, dh_rec,
-                       dc, act, c, c_out, dpre, dc_prev);
+    hipLaunchKernelGGL(k_lstm_bwd<true>, dim3(grid1d(total)), dim3(256), 0, s, total, H, act_um, dh,
+                       dh_rec, dc, act, c, c_out, dpre, dc_prev);
   else
-    hipLaunchKernelGGL(k_lstm_bwd<false>, dim3(grid1d(total)), dim3(256), 0, s, total, H, dh, dh_rec,
-                       dc, act, c, c_out, dpre, dc_prev);
+    hipLaunchKernelGGL(k_lstm_bwd<false>, dim3(grid1d(total)), dim3(256), 0, s, total, H, act_um, dh,
+                       dh_rec, dc, act, c, c_out, dpre, dc_prev);
   return hipGetLastError();
 }
 

@@ -237,10 +237,7 @@ __global__ __launch_bounds__(kST) void k_lstm_seq(SeqArgs A) {
     }, [&](int e, float v) { s_Wx[e] = v; });
   }
   for (int e = tid; e < 128; e += kST) s_b[e] = A.bias ? A.bias[e] : 0.f;
-  for (int e = tid; e < A.nnz; e += kST) {
-    s_val[e] = A.val[e];
-    s_col[e] = static_cast<unsigned short>(A.col[e]);
-  }
+  stage_csr_lds<8, kST>(A.nnz, A.val, A.col, s_val, s_col);
   if (tid == 0) s_abort = 0;
   if (tid < 2 * kQ) (tid < kQ ? slot0 : slot1)[M * kQ + (tid & (kQ - 1))] = 0.f;  // zero row M
   // lane (tile rt, j) owns row order[(wave + 8 rt) * 32 + j]: rows dealt by
@@ -731,25 +728,55 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
   // A operand of MFMA step s, order o: lane (i, q) holds Wh[(16u + i) K + o][g]
   // with g the gate column (s % 4) * 32 + 8q + s / 4 -- the column whose dpre
   // lane (row, q) supplies as the B operand at that step
-  stage_lds<8, kST>(K * 2048, [&](int e) {
-    const int i = e & 15, qq = (e >> 4) & 3, s = (e >> 6) & 31, o = e >> 11;
-    return A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
-  }, [&](int e, float v) { s_W[e] = v; });
-  for (int e = tid; e < A.nnz; e += kST) {
-    s_val[e] = A.tval[e];
-    s_col[e] = static_cast<unsigned short>(A.tcol[e]);
-  }
-  if (tid < kBS) slot[M * kBS + tid] = 0.f;
+  // the prologue's loads in two round trips, not one per staging loop (each
+  // L2 round trip at launch is ~1-2 us, paid by every one of the T-1 launches):
+  // the lanes' rows, Wh and the first kCsr1 * kST CSR entries together, then
+  // the row extents, which need the rows
   // lane (tile rt, jr) owns row order[wave * 128 + 16 rt + jr]
   int rows[kRB], rb[kRB], re[kRB], wl[kRB];
 #pragma unroll
   for (int rt = 0; rt < kRB; ++rt) {
     const int idx = wave * 128 + rt * 16 + jr;
     rows[rt] = idx < M ? A.order[idx] : M;
-    rb[rt] = idx < M ? A.trowptr[rows[rt]] : 0;
-    re[rt] = idx < M ? A.trowptr[rows[rt] + 1] : 0;
-    wl[rt] = wave_max(re[rt] - rb[rt]);
   }
+  constexpr int kWq = K * 2048 / kST, kCsr1 = 16;
+  float wv[kWq], cv[kCsr1];
+  int cc[kCsr1];
+#pragma unroll
+  for (int qd = 0; qd < kWq; ++qd) {
+    const int e = tid + qd * kST;
+    const int i = e & 15, qq = (e >> 4) & 3, s = (e >> 6) & 31, o = e >> 11;
+    wv[qd] = A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
+  }
+#pragma unroll
+  for (int qd = 0; qd < kCsr1; ++qd) {
+    const int e = tid + qd * kST;
+    cv[qd] = e < A.nnz ? A.tval[e] : 0.f;
+    cc[qd] = e < A.nnz ? A.tcol[e] : 0;
+  }
+#pragma unroll
+  for (int rt = 0; rt < kRB; ++rt) {
+    rb[rt] = rows[rt] < M ? A.trowptr[rows[rt]] : 0;
+    re[rt] = rows[rt] < M ? A.trowptr[rows[rt] + 1] : 0;
+  }
+#pragma unroll
+  for (int qd = 0; qd < kWq; ++qd) s_W[tid + qd * kST] = wv[qd];
+#pragma unroll
+  for (int qd = 0; qd < kCsr1; ++qd) {
+    const int e = tid + qd * kST;
+    if (e < A.nnz) {
+      s_val[e] = cv[qd];
+      s_col[e] = static_cast<unsigned short>(cc[qd]);
+    }
+  }
+  if (A.nnz > kCsr1 * kST) {
+    const int rest = A.nnz - kCsr1 * kST;
+    stage_csr_lds<8, kST>(rest, A.tval + kCsr1 * kST, A.tcol + kCsr1 * kST, s_val + kCsr1 * kST,
+                          s_col + kCsr1 * kST);
+  }
+  if (tid < kBS) slot[M * kBS + tid] = 0.f;
+#pragma unroll
+  for (int rt = 0; rt < kRB; ++rt) wl[rt] = wave_max(re[rt] - rb[rt]);
   __syncthreads();
   CG_TS(A.ts, 1);
   f32x4 acc[kRB][K];

@@ -323,8 +323,10 @@ class _Layer(torch.autograd.Function):
         basis_x, hb, Wx, Wh, act, cs, c0, h0, hs = ctx.saved_tensors
         cell, zero_init, fused = ctx.cell, ctx.zero_init, ctx.fused
         H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
-        if cell.seq:  # raises CGError if the forward's launch lost a pair hand-off
-            ops.lstm_seq_fault(plan, wait=True)
+        if cell.seq:  # a fault already known raises now; the blocking check runs
+            # after the backward is queued (a wait here would idle the GPU while
+            # the host queues the backward), before any gradient is returned
+            ops.lstm_seq_fault(plan, wait=False)
         T, N, M, F = ctx.shape
         R = N * M
         dev = act.device
@@ -335,6 +337,12 @@ class _Layer(torch.autograd.Function):
         t_first = 1 if zero_init else 0  # first step whose h-conv ran
         for t in range(T - 1, -1, -1):
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
+            if cell.seq and t < t_first:  # no h-conv at this step: pointwise only, act as stored
+                _, dc, _ = ops.lstm_bwd_step(plan, None if dhs is None else dhs[t], dh_rec, dc,
+                                             act[t], c_prev, cs[t], Wh, K, gates, out_dpre=dpre[t],
+                                             act_unit_major=True, need_dh_prev=False)
+                dh_rec = None
+                continue
             if cell.seq and t >= t_first:
                 # one launch: gates backward, dBasis = dpre Wh^T on MFMA and the
                 # reverse recurrence over L~^T -> the gradient of h_{t-1}
@@ -364,6 +372,8 @@ class _Layer(torch.autograd.Function):
                 dxs, _ = ops.cheb_backward(plan, dpre.view(T * N, M, 4 * H), None, Wx, K,
                                            need_dW=False)
             dx_out = dxs.view(T, N, M, F) if dxs is not None else None
+            if cell.seq:  # raises CGError if the forward's launch lost a pair hand-off
+                ops.lstm_seq_fault(plan, wait=True)
             return (dx_out, None if zero_init else dc, None if zero_init else dh_rec, dWx, dWh, db,
                     None, None, None)
         if T <= t_first:
@@ -389,6 +399,8 @@ class _Layer(torch.autograd.Function):
         dx_out = dxs.view(T, N, M, F) if dxs is not None else None
         dc0 = None if zero_init else dc
         dh0 = None if zero_init else dh_rec
+        if cell.seq:  # raises CGError if the forward's launch lost a pair hand-off
+            ops.lstm_seq_fault(plan, wait=True)
         return dx_out, dc0, dh0, dWx, dWh, db, None, None, None
 
 

@@ -781,13 +781,15 @@ def lstm_seq_forward_x(plan: ChebPlan, xs, Wx, Wh, bias, K: int, gates="referenc
 
 def lstm_bwd_step(plan: ChebPlan, dh, dh_rec, dc, act, c_prev, c_out, Wh, K: int,
                   gates="reference", out_dpre=None, need_dc_prev=True, out_dh_prev=None,
-                  act_unit_major=False):
+                  act_unit_major=False, need_dh_prev=True):
     """One BPTT step of a gconv-LSTM layer in ONE launch (cg_lstm_bwd_step):
     dpre = the gradient of the gate pre-activations, dc_prev, and dh_prev =
     the h-conv's input gradient.  dh / dh_rec / dc / c_prev may be None (= 0).
     act: gate-major [..., 4H] (lstm_cell_forward / lstm_hconv_step) or, with
     act_unit_major, the unit-major [..., H, 4] records of lstm_seq_forward*.
-    Returns (dpre [..., 4H], dc_prev [..., H] or None, dh_prev [..., H])."""
+    need_dh_prev=False: the step ran no h-conv (step 0 of a zero-state layer):
+    the pointwise backward only, dh_prev None.
+    Returns (dpre [..., 4H], dc_prev [..., H] or None, dh_prev [..., H] or None)."""
     _check_dev("act", act)
     _check_dev("c_out", c_out)
     H = int(Wh.shape[1]) // 4
@@ -809,8 +811,10 @@ def lstm_bwd_step(plan: ChebPlan, dh, dh_rec, dc, act, c_prev, c_out, Wh, K: int
         torch.empty(tuple(c_out.shape[:-1]) + (4 * H,), **f32)
     _check_out("dpre", dpre, (R, 4 * H))
     dc_prev = torch.empty(tuple(c_out.shape), **f32) if need_dc_prev else None
-    dh_prev = out_dh_prev if out_dh_prev is not None else torch.empty(tuple(c_out.shape), **f32)
-    _check_out("dh_prev", dh_prev, (R, H))
+    dh_prev = None
+    if need_dh_prev:
+        dh_prev = out_dh_prev if out_dh_prev is not None else torch.empty(tuple(c_out.shape), **f32)
+        _check_out("dh_prev", dh_prev, (R, H))
     _lib.call("cg_lstm_bwd_step", plan.handle, int(N), int(H), int(K), LSTM_GATES[gates], _p(dh),
               _p(dh_rec), _p(dc), _p(act), int(bool(act_unit_major)), _p(c_prev), _p(c_out), _p(Wh),
               _p(dpre), _p(dc_prev),

@@ -407,6 +407,8 @@ int cg_lstm_hconv_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t g
  *   dh / dh_rec / dc / c_prev nullable (= 0), dc_prev nullable.  K <= 4.
  *   act_unit_major: 0 = act [N][M][4H] gate-major (cg_lstm_cell_forward /
  *   cg_lstm_hconv_step), 1 = unit-major [N][M][H][4] (cg_lstm_seq_forward*).
+ *   dh_prev = NULL: the step ran no h-conv (a zero-state layer's step 0): dpre
+ *   and dc_prev only, bitwise cg_lstm_cell_backward on the same act values.
  * ------------------------------------------------------------------------- */
 int cg_lstm_seq_supported(const cg_plan* plan, int32_t H, int32_t K, int32_t* supported);
 int cg_lstm_seq_workspace_bytes(const cg_plan* plan, int32_t N, size_t* bytes);

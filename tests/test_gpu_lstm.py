@@ -301,6 +301,12 @@ def test_bwd_step_equals_pointwise_plus_cheb_backward(dev, K, gates):
             d2, c2, h2 = ops.lstm_bwd_step(plan, a_dh, a_dhr, a_dc, act_um, a_cp, c_out, Wh, K, gates,
                                            act_unit_major=True)
             assert torch.equal(d2, dpre) and torch.equal(c2, dcp) and torch.equal(h2, dhp)
+            # no h-conv at the step (dh_prev NULL): the pointwise part alone, on
+            # either act layout, bitwise the same dpre / dc_prev
+            for a, um in ((act, False), (act_um, True)):
+                d3, c3, h3 = ops.lstm_bwd_step(plan, a_dh, a_dhr, a_dc, a, a_cp, c_out, Wh, K, gates,
+                                               act_unit_major=um, need_dh_prev=False)
+                assert h3 is None and torch.equal(d3, dpre) and torch.equal(c3, dcp)
 
 
 def test_seq_forward_more_samples_than_pairs(dev):
