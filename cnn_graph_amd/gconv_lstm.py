@@ -448,8 +448,8 @@ def layer(cell, xs: torch.Tensor, initial_state=None):
 
     On the one-launch path a lost pair hand-off (cg_lstm_seq_fault) raises
     CGError: here when no gradient will be taken (the outputs go straight to
-    the caller), else at the start of the backward, before any gradient is
-    formed from them (the outputs then hold NaN from the lost step on).
+    the caller), else in the backward, before any gradient is returned (the
+    outputs then hold NaN from the lost step on).
 
     ``cell`` may be a DropoutWrapper: the returned outputs are then dropped
     out, the state (c_T, h_T) is not (DropoutWrapper semantics)."""

@@ -234,18 +234,19 @@ def test_config_E_sequence_path_equals_cell_steps(dev):
     assert O.normwise_err(f64(hs[:, :n]), h_ref) < TOL
 
 
-def test_fused_hstep_equals_unfused(dev):
+@pytest.mark.parametrize("gates", ["reference", "standard"])
+def test_fused_hstep_equals_unfused(dev, gates):
     """The one-launch layer forward + one-launch BPTT steps (hconv='seq':
     cg_lstm_seq_forward / cg_lstm_bwd_step) and the one-launch h-step
     (cg_lstm_hconv_step) against the chebyshev5 + pointwise pair on config E's
     graph at N = 16 (the 2-workgroups-per-sample XCD pairing): states, every
-    gradient."""
+    gradient; both gate sets (each its own sequence-kernel instantiation)."""
     from cnn_graph_amd.gconv_lstm import layer
     Lt, _, M = graph_E()
     T, N, Fin, H, K = 5, 16, 2, 32, 3
     res = {}
     for mode in ("seq", "fused", "unfused"):
-        cell, _ = make_cell(Lt, Fin, H, K, "reference", dev, seed=41, hconv=mode)
+        cell, _ = make_cell(Lt, Fin, H, K, gates, dev, seed=41, hconv=mode)
         g = torch.Generator(device=dev)
         g.manual_seed(3)
         xs = torch.randn((T, N, M, Fin), device=dev, generator=g).requires_grad_()
