@@ -16,7 +16,7 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeou
 tail -1 $OUT/pytest_gpu.txt
 timeout -k 10 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 10 > $OUT/bench.json 2>&1 || { echo BENCH_FAIL; tail -30 $OUT/bench.json; exit 1; }
 tail -1 $OUT/bench.json
-timeout -k 10 500 python scripts/bench_configs.py C1 C2 D E R > $OUT/configs.jsonl 2>&1 || { echo CFG_FAIL; tail -20 $OUT/configs.jsonl; exit 1; }
+timeout -k 10 600 python scripts/bench_configs.py A C1 C2 D E R > $OUT/configs.jsonl 2>&1 || { echo CFG_FAIL; tail -20 $OUT/configs.jsonl; exit 1; }
 grep config $OUT/configs.jsonl
 timeout -k 10 300 python scripts/bench_configs.py C2 D --layout planes > $OUT/configs_planes.jsonl 2>&1 || { echo CFG_PLANES_FAIL; tail -20 $OUT/configs_planes.jsonl; exit 1; }
 grep config $OUT/configs_planes.jsonl
