@@ -423,7 +423,8 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
                            const float* Wx, int Fin, float* xplanes, int64_t xpstride, const float* gx, const float* Wh,
                            const float* bias, const float* h0, const float* c0, float* hs,
                            float* cs, float* act, float* planes, int64_t pstride, int* flags,
-                           int* status, int P, hipStream_t s, int inject_t = -1);
+                           int* status, int P, hipStream_t s, int inject_t = -1,
+                           int max_row_nnz = 1 << 30);
 hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr, const int* tcol,
                              const float* tval, const int* order, int64_t nnzT, const float* dh, const float* dh_rec,
                              const float* dc, const float* act, int act_um, const float* c_prev,

@@ -463,6 +463,7 @@ bool option_valid(int o, int v) {
     case kOptDwDirect: return v >= 0 && v <= 3;
     case kOptDwWaves: return v == 4 || v == 8;
     case kOptClenDy: return v >= 0 && v <= 2;
+    case kOptSeqXpre: return v >= 0 && v <= 2;
     default: return v == 0 || v == 1;
   }
 }
@@ -1672,7 +1673,7 @@ static int lstm_seq_impl(cg_plan* plan, int32_t T, int32_t N, int32_t H, int32_t
   CG_HIP(cg::launch_lstm_seq(gates, T, N, plan->M, K, plan->nnz, plan->rowptr, plan->col, plan->val,
                              plan->lorder, xs, Wx, Fin, xplanes, xplane_stride, gx, Wh, bias, h0,
                              c0, hs, cs, act, planes, plane_stride, flags, plan->seq_fault_dev, P, s,
-                             plan->seq_fault_test));
+                             plan->seq_fault_test, plan->max_row_nnz));
   CG_HIP(hipEventRecord(plan->seq_event, s));
   plan->seq_launched = true;
   return ok();

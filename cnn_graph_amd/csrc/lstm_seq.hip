@@ -946,6 +946,102 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
   CG_TS(A.ts, 4);
 }
 
+// The x basis of every step up front (k_lstm_seq<true>'s pre-pass): each
+// workgroup stages L~ once in LDS and runs the whole K-order recurrence of a
+// few samples' x in LDS, writing plane 0 (= x) and planes 1..K-1.  The
+// arithmetic of k_cheb_step (CSR order from +0, one rounding per product and
+// per add, T_k = 2 acc - T_{k-2}), so the planes are bitwise the streaming
+// steps' -- which took one launch per order, gathering 8-byte rows from L2.
+constexpr int kXT = 1024;
+constexpr int kXL = 16;  // CSR entries of the thread's row kept in registers
+constexpr int kXS = 8;   // samples whose x a workgroup loads at once
+template <int FIN, int K>
+__global__ __launch_bounds__(kXT) void k_xbasis(const int* __restrict__ rowptr,
+                                                const int* __restrict__ col,
+                                                const float* __restrict__ val, int M, int S,
+                                                int spw, const float* __restrict__ xs,
+                                                float* xplanes, int64_t xpstride) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x;
+  const int MF = M * FIN;
+  float* s_T = sm;  // [K][M][FIN]
+  // the thread's row (M <= kXT: one row each) and its CSR entries (at most kXL:
+  // the host checks) in registers for every sample and order (the CSR in LDS
+  // would be read with a row-length stride across the lanes: 8-way bank
+  // conflicts)
+  const int r = tid < M ? tid : M - 1;  // idle lanes mirror the last row; their
+                                        // stores fall outside the descriptors' range
+  const int j0 = rowptr[r], j1 = rowptr[r + 1];
+  float w[kXL];
+  int c[kXL];
+#pragma unroll
+  for (int q = 0; q < kXL; ++q) {
+    w[q] = j0 + q < j1 ? val[j0 + q] : 0.f;
+    c[q] = j0 + q < j1 ? col[j0 + q] * FIN : 0;
+  }
+  const int voff = tid * FIN * 4;  // this lane's bytes in a sample's [M][FIN] slab
+  const int s0 = blockIdx.x * spw, s1 = s0 + spw < S ? s0 + spw : S;
+  // x of a sample and the planes' slabs through buffer descriptors sized to
+  // the slab (an idle lane's access is dropped: no branch, so the compiler
+  // counts the loads and stores exactly and the prefetched x waits only for
+  // what was issued before it)
+  auto slab = [&](const float* p, int smp) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p) + int64_t(smp) * MF, 0, MF * 4,
+                                             0x00020000);
+  };
+  // the x of up to kXS samples loaded together, before any store of theirs:
+  // a load consumed after stores waits for them (vmcnt counts both in order)
+  for (int cb = s0; cb < s1; cb += kXS) {
+    float xr[kXS][FIN];
+#pragma unroll
+    for (int i = 0; i < kXS; ++i) {
+      const __amdgpu_buffer_rsrc_t rx = slab(xs, cb + i < s1 ? cb + i : cb);
+#pragma unroll
+      for (int f = 0; f < FIN; ++f)
+        xr[i][f] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rx, voff + 4 * f, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < kXS; ++i) {
+      const int sm_i = cb + i;
+      if (sm_i >= s1) break;
+      __syncthreads();  // the previous sample's last reads of s_T done
+      {
+        const __amdgpu_buffer_rsrc_t r0 = slab(xplanes, sm_i);
+#pragma unroll
+        for (int f = 0; f < FIN; ++f) {
+          s_T[r * FIN + f] = xr[i][f];  // (idle lanes rewrite the last row's own values)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xr[i][f]), r0, voff + 4 * f, 0, 0);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 1; k < K; ++k) {
+        const float* Tp = s_T + (k - 1) * MF;
+        float acc[FIN];
+#pragma unroll
+        for (int f = 0; f < FIN; ++f) acc[f] = 0.f;
+#pragma unroll
+        for (int q = 0; q < kXL; ++q) {
+          if (j0 + q < j1) {
+#pragma unroll
+            for (int f = 0; f < FIN; ++f) acc[f] = acc[f] + w[q] * Tp[c[q] + f];
+          }
+        }
+        const __amdgpu_buffer_rsrc_t rk = slab(xplanes + int64_t(k) * xpstride, sm_i);
+        __syncthreads();  // every lane's reads of T_{k-1} done before the idle lanes' rewrite
+#pragma unroll
+        for (int f = 0; f < FIN; ++f) {
+          const float o = k >= 2 ? 2.f * acc[f] - s_T[(k - 2) * MF + r * FIN + f] : acc[f];
+          s_T[k * MF + r * FIN + f] = o;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rk, voff + 4 * f, 0, 0);
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 }  // namespace
@@ -985,7 +1081,7 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
                            const float* Wx, int Fin, float* xplanes, int64_t xpstride, const float* gx, const float* Wh,
                            const float* bias, const float* h0, const float* c0, float* hs,
                            float* cs, float* act, float* planes, int64_t pstride, int* flags,
-                           int* status, int P, hipStream_t s, int inject_t) {
+                           int* status, int P, hipStream_t s, int inject_t, int max_row_nnz) {
   if (!lstm_seq_ok(M, kH, K, nnz, xs ? Fin : 0) || N < 1 || T < 1 || P < 1 || P > N ||
       (xs && (Fin < 1 || Fin > 8 || !Wx || !xplanes)) || (!xs && !gx))
     return hipErrorInvalidValue;
@@ -1023,7 +1119,40 @@ hipError_t launch_lstm_seq(int gates, int T, int N, int M, int K, int64_t nnz, c
   // streaming steps over the T*N samples: CSR order from +0, the same values
   // as the in-loop recurrence), unless CG_OPT_SEQ_XPRE = 0 (A/B runs): the loop
   // then only contracts them, and neither workgroup of a pair recomputes them
-  if (xs && seq_xpre()) {
+  const size_t xb_lds = size_t(K) * M * Fin * 4;
+  if (xs && seq_xpre() == 1 && Fin <= 2 && K >= 2 && K <= 4 && M <= kXT && max_row_nnz <= kXL &&
+      xb_lds <= size_t(kLdsBytes)) {
+    // one launch: each workgroup the whole recurrence of a few samples in LDS
+    // [Fin - 1][K - 2]
+    static void (*const xk[2][3])(const int*, const int*, const float*, int, int, int, const float*,
+                                  float*, int64_t) = {{&k_xbasis<1, 2>, &k_xbasis<1, 3>, &k_xbasis<1, 4>},
+                                                      {&k_xbasis<2, 2>, &k_xbasis<2, 3>, &k_xbasis<2, 4>}};
+    static const hipError_t xat = [] {
+      for (auto& row : xk)
+        for (auto* k : row) {
+          const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+          if (e != hipSuccess) return e;
+        }
+      return hipSuccess;
+    }();
+    if (xat != hipSuccess) return xat;
+    auto* xkern = xk[Fin - 1][K - 2];
+    const int S = T * N;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(xkern),
+                                                     kXT, xb_lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int spw = (S + per_cu * cus - 1) / (per_cu * cus);  // every workgroup resident
+    hipLaunchKernelGGL(xkern, dim3((S + spw - 1) / spw), dim3(kXT), xb_lds, s, rowptr, col, val, M,
+                       S, spw, xs, xplanes, xpstride);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    a.xpre = 1;
+  } else if (xs && seq_xpre()) {
     const int64_t R = int64_t(T) * N * M;
     e = hipMemcpyAsync(xplanes, xs, size_t(R) * Fin * sizeof(float), hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return e;

@@ -85,8 +85,10 @@ enum {
   CG_OPT_CLEN_DY = 6,   /* 1: fused-dBasis Clenshaw k_grp_clen_dy, tiles pipelined
                            (default); 2: each order group's tiles up front; 0: row-GEMM
                            dBasis planes + k_grp_clen                                 */
-  CG_OPT_SEQ_XPRE = 7,  /* 1: the gconv-LSTM x basis of all steps formed up front
-                           (default); 0: recomputed inside k_lstm_seq                 */
+  CG_OPT_SEQ_XPRE = 7,  /* 1: the gconv-LSTM x basis of all steps formed up front,
+                           one launch with the recurrence in LDS where it fits
+                           (default); 2: up front by one streaming launch per
+                           order; 0: recomputed inside k_lstm_seq                     */
   CG_OPT_COUNT = 8
 };
 

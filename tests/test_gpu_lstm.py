@@ -310,6 +310,44 @@ def test_bwd_step_equals_pointwise_plus_cheb_backward(dev, K, gates):
                 assert h3 is None and torch.equal(d3, dpre) and torch.equal(c3, dcp)
 
 
+@pytest.mark.parametrize("Fin,K", [(2, 3), (1, 2), (5, 3)])
+def test_seq_x_basis_prepass_modes_bitwise(dev, cg_opts, Fin, K):
+    """The x basis of the one-launch layer forward three ways -- the one-launch
+    LDS pre-pass (k_xbasis, CG_OPT_SEQ_XPRE = 1), one streaming launch per order
+    (= 2), the recurrence inside k_lstm_seq (= 0).  1 and 2: x planes, hs, cs,
+    act and the h planes bitwise equal.  0: the x planes bitwise (the same
+    recurrence), the states to fp32 rounding (the in-loop build contracts x in
+    another MFMA order than the late x contraction of the pre-pass builds)."""
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.plan import ChebPlan
+    Lt, _, M = graph_E()
+    plan = ChebPlan(Lt, device=0)
+    T, N, H = 3, 16, 32
+    g = torch.Generator(device=dev)
+    g.manual_seed(11 * Fin + K)
+    xs = torch.rand((T, N, M, Fin), device=dev, generator=g)
+    Wx = torch.randn((K * Fin, 4 * H), device=dev, generator=g) * 0.1
+    Wh = torch.randn((K * H, 4 * H), device=dev, generator=g) * 0.1
+    b = torch.randn((4 * H,), device=dev, generator=g) * 0.1
+    R = T * N * M
+    out = {}
+    for mode in ("1", "2", "0"):
+        cg_opts("seq_xpre", mode)
+        xpl = torch.full((K, R, Fin), float("nan"), device=dev)
+        pl = torch.zeros((max(K - 1, 1), R, H), device=dev)  # (step 0 has no h-conv: untouched)
+        act_t = torch.empty((R, 4 * H), device=dev)
+        hs, cs, act, _ = ops.lstm_seq_forward_x(plan, xs, Wx, Wh, b, K, out_act=act_t, planes=pl[0],
+                                                plane_stride=R * H, xplanes=xpl)
+        torch.cuda.synchronize()
+        out[mode] = (xpl, hs, cs, act, pl)
+    for a, c in zip(out["1"], out["2"]):
+        assert torch.equal(a, c)
+    assert torch.equal(out["1"][0], out["0"][0])
+    for a, c in zip(out["1"][1:], out["0"][1:]):
+        assert O.normwise_err(a.cpu().numpy(), c.cpu().numpy().astype(np.float64)) < 1e-6
+    assert ops.lstm_seq_fault(plan, wait=True) is False
+
+
 def test_seq_forward_more_samples_than_pairs(dev):
     """N = 136 > the 128 workgroup pairs of a 256-CU chip: pairs take a second
     sample in turn (XCD pairing on).  States and planes equal the per-step
