@@ -356,6 +356,8 @@ int gemm_effective_splits(int Kg, int splits);
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,
                                hipStream_t s);
 // Same fixed-order reduction, then out[i] = out[i] + sum (accumulate != 0).
+hipError_t launch_reduce_slabs3(const float* slab, int nslab, int64_t count, float* out0,
+                                int64_t n0, float* out1, int64_t n01, float* out2, hipStream_t s);
 hipError_t launch_reduce_slabs_acc(const float* slab, int nslab, int64_t count, float* out,
                                    int accumulate, hipStream_t s);
 

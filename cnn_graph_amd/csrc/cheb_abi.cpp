@@ -1358,12 +1358,10 @@ int cg_lstm_weight_grads(int64_t R, int32_t H, int32_t Fin, int32_t K, const flo
   float* comb = reinterpret_cast<float*>(static_cast<char*>(workspace) + slab_bytes);
   CG_HIP(cg::launch_dw_slabs(h_planes, dpre, R, H * K, C, slabs, s, H, h_plane_stride, K, x_planes,
                              Fin, x_plane_stride));
-  CG_HIP(cg::launch_reduce_slabs(slabs, cg::dw_chunks(R), int64_t(rows) * C, comb, s));
-  CG_HIP(hipMemcpyAsync(dWh, comb, size_t(H) * K * C * 4, hipMemcpyDeviceToDevice, s));
-  CG_HIP(hipMemcpyAsync(dWx, comb + size_t(H) * K * C, size_t(Fin) * K * C * 4,
-                        hipMemcpyDeviceToDevice, s));
-  CG_HIP(hipMemcpyAsync(db, comb + size_t(H + Fin) * K * C, size_t(C) * 4, hipMemcpyDeviceToDevice,
-                        s));
+  (void)comb;
+  // the fixed-order slab sums straight into dWh | dWx | db (one launch, no copies)
+  CG_HIP(cg::launch_reduce_slabs3(slabs, cg::dw_chunks(R), int64_t(rows) * C, dWh,
+                                  int64_t(H) * K * C, dWx, int64_t(H + Fin) * K * C, db, s));
   return ok();
 }
 

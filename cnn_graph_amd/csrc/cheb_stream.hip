@@ -891,9 +891,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // a block sums the slabs z = w, w+16, ... for 64 consecutive outputs (one
 // 256-B coalesced load per slab, 8 in flight), then the 16 partial sums are
 // added in wave order through LDS.
-__global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__ slab, int nslab,
-                                                       int64_t count, float* __restrict__ out,
-                                                       int accumulate) {
+template <class OUT>
+__device__ __forceinline__ void reduce_slabs_body(const float* __restrict__ slab, int nslab,
+                                                  int64_t count, OUT&& out) {
 #pragma clang fp contract(off)
   __shared__ float part[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -920,8 +920,33 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__
     float t = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) t = t + part[q][lane];
-    out[i] = accumulate ? out[i] + t : t;
+    out(i, t);
   }
+}
+
+__global__ __launch_bounds__(1024) void k_reduce_slabs(const float* __restrict__ slab, int nslab,
+                                                       int64_t count, float* __restrict__ out,
+                                                       int accumulate) {
+#pragma clang fp contract(off)
+  reduce_slabs_body(slab, nslab, count, [&](int64_t i, float t) {
+    out[i] = accumulate ? out[i] + t : t;
+  });
+}
+
+// the same sums, elements [0, n0) into out0, [n0, n01) into out1, the rest
+// into out2 (the gconv-LSTM's dWh | dWx | db of one slab row block)
+__global__ __launch_bounds__(1024) void k_reduce_slabs3(const float* __restrict__ slab, int nslab,
+                                                        int64_t count, float* __restrict__ out0,
+                                                        int64_t n0, float* __restrict__ out1,
+                                                        int64_t n01, float* __restrict__ out2) {
+  reduce_slabs_body(slab, nslab, count, [&](int64_t i, float t) {
+    if (i < n0)
+      out0[i] = t;
+    else if (i < n01)
+      out1[i - n0] = t;
+    else
+      out2[i - n01] = t;
+  });
 }
 
 }  // namespace
@@ -1216,6 +1241,13 @@ hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int F
 hipError_t launch_reduce_slabs(const float* slab, int nslab, int64_t count, float* out,
                                hipStream_t s) {
   return launch_reduce_slabs_acc(slab, nslab, count, out, 0, s);
+}
+
+hipError_t launch_reduce_slabs3(const float* slab, int nslab, int64_t count, float* out0,
+                                int64_t n0, float* out1, int64_t n01, float* out2, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_slabs3, dim3(unsigned((count + 63) / 64)), dim3(1024), 0, s, slab,
+                     nslab, count, out0, n0, out1, n01, out2);
+  return hipGetLastError();
 }
 
 hipError_t launch_reduce_slabs_acc(const float* slab, int nslab, int64_t count, float* out,
