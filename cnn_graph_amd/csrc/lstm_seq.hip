@@ -700,7 +700,8 @@ struct BStepArgs {
   float* dpre;          // [N][M][128]
   float* dc_prev;       // [N][M][32] or NULL
   float* dh_prev;       // [N][M][32]
-  int dbg;              // ablation build only: 1 no MFMA, 2 no phase-A loads, 4 no recurrence
+  int dbg;              // ablation build only: 1 no MFMA, 2 no phase-A loads, 4 no recurrence,
+                        // 8 no dpre / dc_prev stores
   unsigned long long* ts;  // ablation build: phase stamps (CG_TS), else NULL
 };
 
@@ -847,7 +848,7 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
         dp[3][m] = ref ? d_o * (1.f - o * o) : d_o * (o * (1.f - o));
         dcp[m] = dcn * f;
       }
-      if (own) {
+      if (own && !CG_DBG(A.dbg, 8)) {
         float* dq = A.dpre + rr * 128 + 8 * q;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {

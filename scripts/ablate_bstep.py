@@ -23,7 +23,8 @@ os.environ.setdefault("CG_LIB_PATH", os.path.join(ROOT, "scripts", "dbg", "libch
 from cnn_graph_amd import _lib, ops  # noqa: E402
 from cnn_graph_amd.plan import ChebPlan  # noqa: E402
 
-SETS = {"full": 0, "no_mfma": 1, "no_loads": 2, "no_rec": 4, "no_mfma_loads": 3,
+SETS = {"full": 0, "no_stores": 8, "no_mfma_stores": 9, "no_mfma": 1, "no_loads": 2, "no_rec": 4,
+        "no_mfma_loads": 3,
         "only_rec": 3, "only_loads": 5, "only_mfma": 6, "nothing": 7}
 
 
