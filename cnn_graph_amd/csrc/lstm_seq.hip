@@ -1030,7 +1030,8 @@ __global__ __launch_bounds__(kXT) void k_xbasis(const int* __restrict__ rowptr,
           }
         }
         const __amdgpu_buffer_rsrc_t rk = slab(xplanes + int64_t(k) * xpstride, sm_i);
-        __syncthreads();  // every lane's reads of T_{k-1} done before the idle lanes' rewrite
+        // (T_k is a plane of its own: no barrier between the reads of T_{k-1} and
+        // these writes; idle lanes rewrite the last row with the same values)
 #pragma unroll
         for (int f = 0; f < FIN; ++f) {
           const float o = k >= 2 ? 2.f * acc[f] - s_T[(k - 2) * MF + r * FIN + f] : acc[f];
