@@ -121,6 +121,54 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(int total, int H, int act_um, 
   }
 }
 
+// k_lstm_bwd on unit-major act records (the sequence kernel's), four units
+// per lane: every operand moves in 16-byte accesses (H % 4 == 0, 16-byte
+// aligned operands); per element the expressions of k_lstm_bwd, bitwise
+template <bool REF>
+__global__ __launch_bounds__(256) void k_lstm_bwd_um4(int total4, int H, const float* __restrict__ dh,
+                                                      const float* __restrict__ dh_rec,
+                                                      const float* __restrict__ dc,
+                                                      const float* __restrict__ act,
+                                                      const float* __restrict__ c,
+                                                      const float* __restrict__ c_out,
+                                                      float* __restrict__ dpre,
+                                                      float* __restrict__ dc_prev) {
+#pragma clang fp contract(off)
+  const int H4 = H >> 2;
+  for (int e4 = blockIdx.x * 256 + threadIdx.x; e4 < total4; e4 += gridDim.x * 256) {
+    const int r = e4 / H4, j0 = (e4 - r * H4) * 4;
+    const int64_t e = int64_t(r) * H + j0;  // element (r, j0)
+    auto ld4 = [&](const float* p) {
+      return p ? *reinterpret_cast<const float4*>(p + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    const float4 cp4 = ld4(c), co4 = ld4(c_out), dh4 = ld4(dh), dr4 = ld4(dh_rec), dc4 = ld4(dc);
+    float dp[4][4], dcp[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 a = *reinterpret_cast<const float4*>(act + int64_t(r) * 4 * H + 4 * (j0 + u));
+      const float z = a.x, i = a.y, f = a.z, o = a.w;
+      const float cp = (&cp4.x)[u];
+      const float tc = gate_tanh((&co4.x)[u]);
+      float dhv = dh ? (&dh4.x)[u] : 0.f;
+      if (dh_rec) dhv = dhv + (&dr4.x)[u];
+      float dcn = dhv * o * (1.f - tc * tc);
+      if (dc) dcn = dcn + (&dc4.x)[u];
+      const float d_o = dhv * tc;
+      const float d_i = dcn * z, d_z = dcn * i, d_f = dcn * cp;
+      dp[0][u] = REF ? d_z * (1.f + z * z) : d_z * (1.f - z * z);
+      dp[1][u] = d_i * (i * (1.f - i));
+      dp[2][u] = d_f * (f * (1.f - f));
+      dp[3][u] = REF ? d_o * (1.f - o * o) : d_o * (o * (1.f - o));
+      dcp[u] = dcn * f;
+    }
+    const int64_t g0 = int64_t(r) * 4 * H + j0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(dpre + g0 + g * H) = make_float4(dp[g][0], dp[g][1], dp[g][2], dp[g][3]);
+    if (dc_prev) *reinterpret_cast<float4*>(dc_prev + e) = make_float4(dcp[0], dcp[1], dcp[2], dcp[3]);
+  }
+}
+
 // Column sums of A [R][C] as per-chunk partial slabs slab[chunk][C]: block
 // (chunk, 64-column tile) = 4 waves; wave w sums rows c0 + w, c0 + w + 4, ...
 // of the chunk for its 64 columns (one coalesced 256-B load per row), then the
@@ -170,6 +218,18 @@ hipError_t launch_lstm_bwd(int gates, int64_t R, int H, const float* dh, const f
                            const float* act, const float* c, const float* c_out, float* dpre,
                            float* dc_prev, hipStream_t s, int act_um) {
   const int total = int(R * H);
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (act_um && H % 4 == 0 && al(dh) && al(dh_rec) && al(dc) && al(act) && al(c) && al(c_out) &&
+      al(dpre) && al(dc_prev)) {
+    const int total4 = total / 4;
+    if (gates == 0)
+      hipLaunchKernelGGL(k_lstm_bwd_um4<true>, dim3(grid1d(total4)), dim3(256), 0, s, total4, H, dh,
+                         dh_rec, dc, act, c, c_out, dpre, dc_prev);
+    else
+      hipLaunchKernelGGL(k_lstm_bwd_um4<false>, dim3(grid1d(total4)), dim3(256), 0, s, total4, H, dh,
+                         dh_rec, dc, act, c, c_out, dpre, dc_prev);
+    return hipGetLastError();
+  }
   if (gates == 0)
     hipLaunchKernelGGL(k_lstm_bwd<true>, dim3(grid1d(total)), dim3(256), 0, s, total, H, act_um, dh,
                        dh_rec, dc, act, c, c_out, dpre, dc_prev);
