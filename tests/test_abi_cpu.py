@@ -47,6 +47,11 @@ def test_options_roundtrip_and_validation(built_lib):
     assert h.cg_set_option(99, 1) == _lib.CG_ERR_ARG
     assert h.cg_set_option(_lib.OPTIONS["dw_waves"], 5) == _lib.CG_ERR_ARG
     assert h.cg_set_option(_lib.OPTIONS["spmm_pw"], 2) == _lib.CG_ERR_ARG
+    # the x-basis pre-pass: 0 in-loop, 1 one LDS launch (default), 2 per-order launches
+    assert _lib.get_option("seq_xpre") == 1
+    with _lib.options(seq_xpre=2):
+        assert _lib.get_option("seq_xpre") == 2
+    assert h.cg_set_option(_lib.OPTIONS["seq_xpre"], 3) == _lib.CG_ERR_ARG
     assert h.cg_get_option(0, None) == _lib.CG_ERR_ARG
     assert h.cg_plan_set_seq_fault_test(None, 1) == _lib.CG_ERR_ARG
 
