@@ -39,6 +39,11 @@
 //   processed by the same pairs in turn.  The grid never exceeds the
 //   occupancy query's resident workgroups (checked at launch).
 //
+// k_xbasis (the x basis of every step, one launch before k_lstm_seq<true>)
+//   One 1024-thread workgroup per CU runs the whole K-order recurrence of a
+//   few samples' x in LDS, each thread's CSR row in registers; planes bitwise
+//   the streaming k_cheb_step launches' (CG_OPT_SEQ_XPRE = 2 keeps those).
+//
 // k_lstm_bstep (backward, one launch per step, two workgroups per sample)
 //   dpre = TF autodiff of the pointwise update (the expressions of
 //   lstm.hip::k_lstm_bwd, so dpre is bitwise the unfused kernel's), then
