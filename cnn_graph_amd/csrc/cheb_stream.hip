@@ -1024,7 +1024,40 @@ hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const floa
   const int NT = (Nc + 31) / 32;
   const size_t lds = size_t(2) * a.KC2 * NT * 32 * 4;
   const int64_t ntiles = (R + 127) / 128;
-  const unsigned gx = unsigned(ntiles < 1024 ? ntiles : 1024);
+  // every chunk 16 contiguous in-range floats, at least 3 of them per half
+  const bool pf = a.vecA && a.KC2 % 16 == 0 && 2 * a.KC2 <= Kc && a.KC2 / 16 >= 3;
+  // the persistent blocks: as many as are resident at once (a grid beyond that
+  // runs its last blocks as a tail at a fraction of the chip: config D's y GEMM
+  // had 1 024 blocks for 768 resident slots), at most 1 024
+  unsigned gx = unsigned(ntiles < 1024 ? ntiles : 1024);
+  {
+    static int resident[2][9] = {};  // [pf][NT] blocks resident on the whole chip (0 = unknown)
+    const int nt = NT < 8 ? NT : 8;
+    int& res_blocks = resident[pf ? 1 : 0][nt];
+    if (res_blocks == 0) {
+      const void* k = nullptr;
+#define CG_RGK(n)                                                                              \
+  case n:                                                                                      \
+    k = pf ? reinterpret_cast<const void*>(&k_rowgemm<n, true>)                                \
+           : reinterpret_cast<const void*>(&k_rowgemm<n, false>);                              \
+    break;
+      switch (nt) { CG_RGK(1) CG_RGK(2) CG_RGK(3) CG_RGK(4) CG_RGK(5) CG_RGK(6) CG_RGK(7) default: CG_RGK(8) }
+#undef CG_RGK
+      int per_cu = 0, cus = 0, dev = 0;
+      (void)hipGetDevice(&dev);
+      if (lds > size_t(64) * 1024)
+        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds) == hipSuccess &&
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+          per_cu > 0 && cus > 0)
+        res_blocks = per_cu * cus;
+      else
+        res_blocks = -1;  // unknown: keep the 1 024 cap
+    }
+    if (res_blocks > 0 && int64_t(res_blocks) * planes >= 1 && gx > unsigned(res_blocks) / unsigned(planes) &&
+        unsigned(res_blocks) / unsigned(planes) >= 1)
+      gx = unsigned(res_blocks) / unsigned(planes);
+  }
   const dim3 grid(gx, unsigned(planes)), block(256);
   if (lds > size_t(64) * 1024) {
     static hipError_t attr[8] = {};
@@ -1056,8 +1089,6 @@ hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const floa
     }
     if (attr[(NT < 8 ? NT : 8) - 1] != hipSuccess) return attr[(NT < 8 ? NT : 8) - 1];
   }
-  // every chunk 16 contiguous in-range floats, at least 3 of them per half
-  const bool pf = a.vecA && a.KC2 % 16 == 0 && 2 * a.KC2 <= Kc && a.KC2 / 16 >= 3;
 #define CG_RG(nt)                                                                 \
   case nt:                                                                        \
     if (pf) hipLaunchKernelGGL((k_rowgemm<nt, true>), grid, block, lds, s, a);    \
