@@ -330,12 +330,219 @@ def spawn_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
+def batch_split(args, rank, world):
+    """(per-rank batch, whole-job batch, strong?) for --batch / --global-batch."""
+    if args.global_batch is not None:
+        lo, hi = cdist.shard(args.global_batch, rank, world)
+        if hi - lo < 1:
+            sys.exit(f"bench.py: global batch {args.global_batch} < {world} ranks")
+        return hi - lo, args.global_batch, True
+    return args.batch, args.batch * world, False
+
+
+def make_exchange(args, world, local):
+    """The gradient exchange of configs D / E: (comm object with allreduce_sum_
+    and world, rccl_nranks or None).  RCCL (cg_allreduce_sum_f32 on the compute
+    stream) by default; torch.distributed (gloo in the one-GPU world-2 test)
+    with --allreduce torch."""
+    if not (world > 1 or args.force_allreduce):
+        return None, None
+    if args.allreduce == "rccl":
+        comm = cdist.RcclComm(local)
+        n = comm.nranks()
+        if n != world:
+            sys.exit(f"bench.py: RCCL communicator spans {n} ranks, expected {world}")
+        return comm, n
+    return cdist.TorchComm(), None
+
+
+def timed_region(step, steps, warmup, world, dev):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize
+    on both sides; the max over ranks of the elapsed seconds."""
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed, = max_over_ranks([elapsed], dev)
+    return elapsed
+
+
+def train_step_d(args, N, world, local, dev, comm, rank):
+    """Config D's data-parallel chebyshev5 training step (BASELINE configs[3]):
+    the seeded Chung-Lu graph (scripts/synth_graphs.py, M = 2^18, nnz(L~) =
+    4 189 524), Fin = Fout = 64, K = 3, N samples per rank; forward, backward
+    (dx, dW), the all-reduce of dW (192 x 64 floats = 48 KB) when there is an
+    exchange, then cg_adam_update (the unfused schedule of dp_step: one
+    12 288-float launch against a ~0.2 s step).  Returns (step fn, info dict)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import synth_graphs
+    from cnn_graph_amd.graph import rescale_L
+    K, Fin, Fout = 3, 64, 64
+    Lt = rescale_L(synth_graphs.config_d_laplacian(), 2)
+    plan = ChebPlan(Lt, device=local)
+    layout = ops.basis_layout_for(plan, N, Fin, K, Fout)
+    runner = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=layout)
+    g = torch.Generator(device=dev)
+    g.manual_seed(2017 + rank)
+    if layout == "planes":  # the input lives in plane 0 of the basis (T_0 read in place)
+        x = runner.input_plane()
+        x.copy_(torch.rand(x.shape, device=dev, generator=g))
+    else:
+        x = torch.rand((N, plan.M, Fin), device=dev, generator=g)
+    W = truncated_normal_(torch.empty((Fin * K, Fout), device=dev), 0.1)
+    cdist.broadcast_parameters([W])
+    dy = torch.randn((N, plan.M, Fout), device=dev, generator=g)
+    allreduce = None
+    if comm is not None:
+        def allreduce(s):
+            comm.allreduce_sum_(runner.dW, s)
+    trainer = ChebTrainStep(runner, x, dy, W, world=world, allreduce=allreduce, schedule="unfused")
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(i):
+        trainer.step(i, stream)
+
+    def kernels():
+        fwd = burst_ms(lambda: runner.forward(x, trainer.W[0], stream=stream), reps=2, rounds=3)
+        bwd = burst_ms(lambda: runner.backward(dy, trainer.W[0], stream=stream), reps=2, rounds=3)
+        bf, bb, _ = algorithmic_bytes(plan.M, plan.nnz, N * Fin, K)
+        return {"fwd": {"kernel": "stream_fwd (k_cheb_step x 2 + k_rowgemm)", "ms": fwd, "alg_bytes": bf},
+                "bwd": {"kernel": "stream_bwd (k_clenshaw_step + dBasis/dW GEMMs)", "ms": bwd,
+                        "alg_bytes": bb}}
+
+    info = {"workload": "config D: seeded Chung-Lu power-law graph, M=262144, K=3, Fin=64, Fout=64, "
+                        "chebyshev5 fwd+bwd" + (" + dW all-reduce" if comm is not None else "") + " + Adam",
+            "M": plan.M, "nnz": plan.nnz, "K": K, "Fin": Fin, "Fout": Fout,
+            "path": plan.query_path(N, Fin, K, Fout), "basis_layout": layout,
+            "grad_bucket_bytes": 4 * Fin * K * Fout, "adam": "cg_adam_update"}
+    cpu = lambda: cpu_baseline_filter("D", Lt, 1, N, Fin, K, Fout, seconds=args.cpu_seconds,  # noqa: E731
+                                      warmup=1, min_passes=3)
+    return step, info, kernels, cpu, "bytes"
+
+
+def train_step_e(args, N, world, local, dev, comm, rank):
+    """Config E's data-parallel gconv-LSTM training step (BASELINE configs[4]):
+    gconv_lstm.GLSTMModel -- inference_glstm = glstm_layer (one GConvLSTMCell,
+    T = 12, K = 3, Fin = 2, H = 32, DropoutWrapper keep_prob 0.8) + fc_layer
+    (lib/gconv_lstm.py:271-281, :609-636) -- MSE, backward through time, ONE
+    all-reduce of the flat gradient bucket (13 376 floats = 53.5 KB) when there
+    is an exchange, then Adam, on config E's 1 024-vertex grid graph; N
+    samples per rank."""
+    from cnn_graph_amd.gconv_lstm import GLSTMModel
+    T, Fin, H, K, Fout = 12, 2, 32, 3, 2
+    with np.load(os.path.join(ROOT, "tests", "golden", "golden_E.npz"), allow_pickle=False) as z:
+        M = int(z["M"])
+        Lt = scipy.sparse.csr_matrix((z["Lt_val"], z["Lt_col"], z["Lt_rowptr"]), shape=(M, M))
+    L = (Lt + scipy.sparse.identity(M, dtype=np.float32, format="csr")).tocsr()  # rescale_L(L, 2) = L~
+    model = GLSTMModel(L, N, T, Fin, num_hidden=H, K=K, out_features=Fout, keep_prob=0.8,
+                       device=dev, seed=2017, comm=comm)
+    cdist.broadcast_parameters([model.flat])
+    g = torch.Generator(device=dev)
+    g.manual_seed(2017 + rank)
+    x = torch.rand((N, M, Fin * T), device=dev, generator=g)   # [N, M, F*T] as the reference feeds it
+    labels = torch.rand((N, M, Fout), device=dev, generator=g)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(i):
+        model.train_step(x, labels, stream)
+
+    def kernels():
+        with torch.no_grad():
+            fwd = burst_ms(lambda: model.forward(x), reps=5, rounds=3)
+        # gate contractions of one forward: T steps x N samples x M rows x
+        # (K*Fin + K*H) inputs x 4H gate columns, 2 flops each
+        flops = 2.0 * T * N * M * (K * Fin + K * H) * 4 * H
+        return {"fwd": {"kernel": "glstm_layer forward (k_xbasis + k_lstm_seq) + fc cheb_conv",
+                        "ms": fwd, "alg_flops": flops}}
+
+    info = {"workload": "config E: gconv-LSTM (GLSTMModel: glstm_layer + fc_layer), grid graph M=1024, "
+                        "T=12, K=3, Fin=2, H=32, keep_prob 0.8, MSE + BPTT"
+                        + (" + gradient all-reduce" if comm is not None else "") + " + Adam",
+            "M": M, "T": T, "K": K, "Fin": Fin, "H": H, "Fout": Fout,
+            "grad_bucket_bytes": 4 * model.flat.numel(), "adam": "cg_adam_update (flat buffer)"}
+    cpu = lambda: cpu_baseline_lstm(Lt, 8, N, T, Fin, H, K, seconds=args.cpu_seconds)  # noqa: E731
+    return step, info, kernels, cpu, "flops"
+
+
+def run_config_de(args, rank, world, local, dev, json_fd):
+    """--config D / E: the config's training step through the contract's timed
+    region (barrier + synchronize both sides, max over ranks); one JSON line on
+    rank 0 with n_gpus, batch_per_gpu, global_batch and rccl_nranks."""
+    N, N_global, strong = batch_split(args, rank, world)
+    comm, rccl_nranks = make_exchange(args, world, local)
+    build = train_step_d if args.config == "D" else train_step_e
+    step, info, kernels, cpu, bound = build(args, N, world, local, dev, comm, rank)
+    try:
+        elapsed = timed_region(step, args.steps, args.warmup, world, dev)
+    except Exception:
+        if isinstance(comm, cdist.RcclComm) and comm.async_error(abort=True):
+            sys.exit(f"bench.py: RCCL asynchronous error on rank {rank}")
+        raise
+    kern = kernels()
+    if bound == "bytes":
+        dom = max(kern, key=lambda k: kern[k]["ms"])
+        ach = kern[dom]["alg_bytes"] / (kern[dom]["ms"] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": kern[dom]["kernel"], "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": None, "alg_bytes_per_launch": kern[dom]["alg_bytes"],
+                "avg_launch_ms": round(kern[dom]["ms"], 4),
+                "timing": "HIP events on the launch stream around back-to-back calls"}
+    else:
+        k = kern["fwd"]
+        ach = k["alg_flops"] / (k["ms"] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": k["kernel"], "achieved": round(ach, 2),
+                "peak": MFMA_F32_PEAK_TF, "unit": "TFLOP/s", "frac": round(ach / MFMA_F32_PEAK_TF, 4),
+                "traffic": None, "alg_flops_per_call": k["alg_flops"], "avg_call_ms": round(k["ms"], 4),
+                "timing": "HIP events on the launch stream around back-to-back forward calls"}
+    info.update({"batch_per_gpu": N, "global_batch": N_global, "parallelism": f"dp{world}",
+                 "allreduce": (args.allreduce if comm is not None else None),
+                 "dist_backend": (dist.get_backend() if world > 1 else None),
+                 "rccl_nranks": rccl_nranks, "launch": "eager C-ABI calls per step"})
+    out = {"metric": "Chebyshev-K fwd+bwd samples/sec", "value": round(N_global * args.steps / elapsed, 2),
+           "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+           "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic (seeded inputs / labels, truncated-normal weights)",
+           "config": info, "roofline": roof,
+           "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                       for k, v in kern.items()}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu()
+    if rank == 0:
+        ctypes.CDLL(None).fflush(None)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=256, help="samples per GPU (weak scaling)")
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default B 200, D 10, E 50)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default B 20, D 2, E 5)")
+    ap.add_argument("--config", default="B", choices=["B", "D", "E"],
+                    help="B (default, the headline: BASELINE configs[1]); D: the 2^18-vertex "
+                         "power-law graph, Fin = Fout = 64, K = 3, 256 per GPU (configs[3]: 2 048 "
+                         "over 8); E: the gconv-LSTM model, T = 12, 128 per GPU (configs[4]: 512 "
+                         "over 4).  D and E time their own training step (train_step_d / "
+                         "train_step_e below) through the same torchrun / barrier / max-over-ranks path")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="samples per GPU (weak scaling; default 256 for B and D, 128 for E)")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="fixed whole-job batch sharded over the ranks (strong scaling)")
     ap.add_argument("--path", default="auto", choices=["auto", "resident", "stream"])
@@ -355,12 +562,19 @@ def main():
                     help="capture the K timed steps into one HIP graph before the timed region and "
                          "replay it there (every kernel of every step still runs); measured 0-1 %% "
                          "slower than eager launches on config B (profiles/r03_graph), so off")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="kernel-selection option name=value (cg_set_option) for A/B runs, "
+                         "e.g. fast_rpl=2; the defaults are the measured-faster kernels")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "gloo"],
                     help="test only: gloo runs the N > 1 entry path (torchrun, init, barrier, max over "
                          "ranks) with every rank on GPU local_rank mod the visible GPUs, e.g. two "
                          "ranks on a one-GPU box (needs --allreduce torch: RCCL refuses two ranks "
                          "on one device); auto = nccl (RCCL) whenever a GPU is visible")
     args = ap.parse_args()
+    dflt = {"B": (200, 20, 256), "D": (10, 2, 256), "E": (50, 5, 128)}[args.config]
+    args.steps = dflt[0] if args.steps is None else args.steps
+    args.warmup = dflt[1] if args.warmup is None else args.warmup
+    args.batch = dflt[2] if args.batch is None else args.batch
     if args.dist_backend == "gloo" and args.allreduce != "torch":
         sys.exit("bench.py: --dist-backend gloo needs --allreduce torch")
 
@@ -380,6 +594,13 @@ def main():
         local %= torch.cuda.device_count()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    for kv in args.opt:
+        name, val = kv.split("=")
+        _lib.set_option(name, int(val))
+    if args.config != "B":
+        run_config_de(args, rank, world, local, dev, json_fd)
+        return
 
     K, Fin, Fout = 25, 1, 32
     L, fake = load_config_b()
@@ -568,6 +789,7 @@ def main():
                    "allreduce": (args.allreduce if exchange else None),
                    "dist_backend": (dist.get_backend() if world > 1 else None),
                    "rccl_nranks": rccl_nranks,
+                   "options": dict(kv.split("=") for kv in args.opt) or None,
                    "launch": ("one HIP graph replay of the K captured steps" if graph is not None
                               else "eager C-ABI calls per step"),
                    "adam": ("fused into the dW reduction (cg_cheb_backward_adam)" if fuse_adam

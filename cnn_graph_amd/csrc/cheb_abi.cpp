@@ -457,13 +457,14 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
 namespace cg {
 namespace {
 // CG_OPT_* values (defaults: the measured-faster kernels) and their ranges
-std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}};
+std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}, {1}};
 bool option_valid(int o, int v) {
   switch (o) {
     case kOptDwDirect: return v >= 0 && v <= 3;
     case kOptDwWaves: return v == 4 || v == 8;
     case kOptClenDy: return v >= 0 && v <= 2;
     case kOptSeqXpre: return v >= 0 && v <= 2;
+    case kOptFastRpl: return v == 1 || v == 2;
     default: return v == 0 || v == 1;
   }
 }
@@ -1032,6 +1033,16 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   }
   if (!dW) return ok();
   if (fused) nslab_ready = N;
+  // small problems (config A): dW in one block, no slabs and no reduction
+  // launch (with Adam: the one result is the single slab of the fused reduction)
+  if (!nslab_ready && layout != CG_BASIS_ORDERS && cg::dw_small_ok(R, FinK, Fout) &&
+      !(cg::debug_flags() & (1 << 22))) {
+    const int pl = layout == CG_BASIS_PLANES ? Fin : 0;
+    CG_HIP(cg::launch_dw_small(basis, dy, R, FinK, Fout, adam ? slabs : dW, s, pl,
+                               pl ? int64_t(R) * Fin : 0, K));
+    if (!adam) return ok();
+    nslab_ready = 1;
+  }
   if (!nslab_ready) CG_HIP(launch_dw(s));
   const int nslab = nslab_ready ? nslab_ready : chunks;
   if (adam)  // reduction + optimizer step in one launch (no exchange in between)

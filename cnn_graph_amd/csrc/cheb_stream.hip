@@ -21,6 +21,7 @@
 // The SpMM accumulates sequentially in CSR order with fp contraction off, so
 // the basis is bit-identical to the resident path and to lib/graph.py::chebyshev.
 #include "cg_internal.h"
+#include "occupancy_cache.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -949,7 +950,77 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs3(const float* __restrict_
   });
 }
 
+// dW = basis^T dy of a small problem in one block: thread t owns output
+// o = t mod nout (j = o / Fout, f = o mod Fout) and rows r = g, g + G, ... of
+// group g = t / nout (G = 1024 / nout groups), 8 rows' loads in flight before
+// their 8 mul / add pairs; then thread o sums the G group partials in group
+// order.  Fixed order, so bitwise reproducible (another grouping than the
+// slabs': dW agrees with them to fp32 rounding).  Basis column j = fin*K + k
+// of row r: rows layout basis[r*FinK + j], planes layout
+// basis[k*pl_stride + r*pl_fin + fin].
+__global__ __launch_bounds__(1024) void k_dw_small(const float* __restrict__ basis,
+                                                   const float* __restrict__ dy, int64_t R,
+                                                   int FinK, int Fout, float* __restrict__ out,
+                                                   int pl_fin, int64_t pl_stride, int K) {
+#pragma clang fp contract(off)
+  __shared__ float part[1024];
+  const int t = threadIdx.x;
+  const int nout = FinK * Fout;
+  const int G = 1024 / nout;
+  float s = 0.f;
+  if (t < G * nout) {
+    const int o = t % nout, g = t / nout;
+    const int j = o / Fout, f = o - j * Fout;
+    const float* pa;
+    int64_t sa;
+    if (pl_fin > 0) {
+      const int fin = j / K, k = j - fin * K;
+      pa = basis + int64_t(k) * pl_stride + fin;
+      sa = pl_fin;
+    } else {
+      pa = basis + j;
+      sa = FinK;
+    }
+    const float* pb = dy + f;
+    for (int64_t r0 = g; r0 < R; r0 += 8 * int64_t(G)) {
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t r = r0 + int64_t(u) * G;
+        a[u] = r < R ? pa[r * sa] : 0.f;
+        b[u] = r < R ? pb[r * Fout] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r0 + int64_t(u) * G < R) s = s + a[u] * b[u];
+    }
+  }
+  part[t] = s;
+  __syncthreads();
+  if (t < nout) {
+    float tot = 0.f;
+    for (int g = 0; g < G; ++g) tot = tot + part[g * nout + t];
+    out[t] = tot;
+  }
+}
+
 }  // namespace
+
+bool dw_small_ok(int64_t R, int FinK, int Fout) {
+  const int64_t nout = int64_t(FinK) * Fout;
+  if (nout < 1 || nout > 1024) return false;
+  const int64_t G = 1024 / nout;
+  return R <= 256 * G;  // at most 256 rows per thread
+}
+
+hipError_t launch_dw_small(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
+                           float* out, hipStream_t s, int pl_fin, int64_t pl_stride, int K) {
+  if (!dw_small_ok(R, FinK, Fout) || (pl_fin > 0 && (K < 1 || FinK != pl_fin * K)))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_dw_small, dim3(1), dim3(1024), 0, s, basis, dy, R, FinK, Fout, out, pl_fin,
+                     pl_stride, K);
+  return hipGetLastError();
+}
 
 hipError_t launch_cheb_step(const int* rowptr, const int* col, const float* val, const int* rperm,
                             const float* Tp, const float* Tpp, float* Tout, const float* x,
@@ -1029,40 +1100,34 @@ hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const floa
   // the persistent blocks: as many as are resident at once (a grid beyond that
   // runs its last blocks as a tail at a fraction of the chip: config D's y GEMM
   // had 1 024 blocks for 768 resident slots), at most 1 024
-  unsigned gx = unsigned(ntiles < 1024 ? ntiles : 1024);
+  unsigned gx;
   {
-    static int resident[2][9] = {};  // [pf][NT] blocks resident on the whole chip (0 = unknown)
     const int nt = NT < 8 ? NT : 8;
-    int& res_blocks = resident[pf ? 1 : 0][nt];
-    if (res_blocks == 0) {
-      const void* k = nullptr;
+    const void* k = nullptr;
 #define CG_RGK(n)                                                                              \
   case n:                                                                                      \
     k = pf ? reinterpret_cast<const void*>(&k_rowgemm<n, true>)                                \
            : reinterpret_cast<const void*>(&k_rowgemm<n, false>);                              \
     break;
-      switch (nt) { CG_RGK(1) CG_RGK(2) CG_RGK(3) CG_RGK(4) CG_RGK(5) CG_RGK(6) CG_RGK(7) default: CG_RGK(8) }
+    switch (nt) { CG_RGK(1) CG_RGK(2) CG_RGK(3) CG_RGK(4) CG_RGK(5) CG_RGK(6) CG_RGK(7) default: CG_RGK(8) }
 #undef CG_RGK
-      int per_cu = 0, cus = 0, dev = 0;
-      (void)hipGetDevice(&dev);
-      if (lds > size_t(64) * 1024)
-        (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, lds) == hipSuccess &&
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-          per_cu > 0 && cus > 0)
-        res_blocks = per_cu * cus;
-      else
-        res_blocks = -1;  // unknown: keep the 1 024 cap
-    }
-    if (res_blocks > 0 && int64_t(res_blocks) * planes >= 1 && gx > unsigned(res_blocks) / unsigned(planes) &&
-        unsigned(res_blocks) / unsigned(planes) >= 1)
-      gx = unsigned(res_blocks) / unsigned(planes);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    // keyed on (device, kernel, threads, dynamic LDS): the LDS follows Kc
+    static ResidentCache cache;
+    const int res_blocks = cache.get(dev, k, 256, lds, [&](const void* kf, int thr, size_t l, int* per_cu,
+                                                           int* cus) {
+      if (l > size_t(64) * 1024)
+        (void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kf, thr, l) == hipSuccess &&
+             hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
+    });
+    gx = persistent_grid(ntiles, res_blocks, planes);
   }
   const dim3 grid(gx, unsigned(planes)), block(256);
   if (lds > size_t(64) * 1024) {
-    static hipError_t attr[8] = {};
-    static bool set = false;
-    if (!set) {
+    // once per process, thread-safe (a function-local static's initialiser)
+    static const hipError_t attr = [] {
       const void* ks[16] = {reinterpret_cast<const void*>(&k_rowgemm<1, false>),
                             reinterpret_cast<const void*>(&k_rowgemm<2, false>),
                             reinterpret_cast<const void*>(&k_rowgemm<3, false>),
@@ -1079,15 +1144,13 @@ hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const floa
                             reinterpret_cast<const void*>(&k_rowgemm<6, true>),
                             reinterpret_cast<const void*>(&k_rowgemm<7, true>),
                             reinterpret_cast<const void*>(&k_rowgemm<8, true>)};
-      for (int q = 0; q < 8; ++q) {
-        attr[q] = hipFuncSetAttribute(ks[q], hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        if (attr[q] == hipSuccess)
-          attr[q] = hipFuncSetAttribute(ks[q + 8], hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        kLdsBytes);
+      for (const void* k : ks) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        if (e != hipSuccess) return e;
       }
-      set = true;
-    }
-    if (attr[(NT < 8 ? NT : 8) - 1] != hipSuccess) return attr[(NT < 8 ? NT : 8) - 1];
+      return hipSuccess;
+    }();
+    if (attr != hipSuccess) return attr;
   }
 #define CG_RG(nt)                                                                 \
   case nt:                                                                        \
@@ -1135,8 +1198,13 @@ hipError_t launch_gemm_f32(bool trans_a, bool trans_b, int Mg, int Ng, int Kg, c
 }
 
 int dw_chunks(int64_t R) {
-  // ~512 rows per chunk, at most 1024 chunks (slab bytes stay <= 1024*FinK*Fout*4)
+  // ~512 rows per chunk, at most 1024 chunks (slab bytes stay <= 1024*FinK*Fout*4).
+  // Small problems (fewer than 32 such chunks) take 32-row chunks instead: a
+  // chunk is a serial chain of 16-row LDS batches, so config A's 3 200 rows in
+  // 7 chunks of 457 took 29.8 us of a 48 us backward (profiles/r06b, kernel
+  // trace of bench_configs A); in 100 chunks of 32 rows they are two batches
   int64_t c = (R + 511) / 512;
+  if (c < 32) c = (R + 31) / 32 < 512 ? (R + 31) / 32 : 512;
   if (c > 1024) c = 1024;
   return int(c < 1 ? 1 : c);
 }

@@ -976,8 +976,11 @@ __global__ __launch_bounds__(kXT) void k_xbasis(const int* __restrict__ rowptr,
   // the host checks) in registers for every sample and order (the CSR in LDS
   // would be read with a row-length stride across the lanes: 8-way bank
   // conflicts)
-  const int r = tid < M ? tid : M - 1;  // idle lanes mirror the last row; their
-                                        // stores fall outside the descriptors' range
+  const bool live = tid < M;
+  const int r = live ? tid : M - 1;  // idle lanes mirror the last row's CSR; their
+                                     // global stores fall outside the descriptors'
+                                     // range and they write no LDS (their x is the
+                                     // out-of-range 0, not row M-1's)
   const int j0 = rowptr[r], j1 = rowptr[r + 1];
   float w[kXL];
   int c[kXL];
@@ -1016,7 +1019,7 @@ __global__ __launch_bounds__(kXT) void k_xbasis(const int* __restrict__ rowptr,
         const __amdgpu_buffer_rsrc_t r0 = slab(xplanes, sm_i);
 #pragma unroll
         for (int f = 0; f < FIN; ++f) {
-          s_T[r * FIN + f] = xr[i][f];  // (idle lanes rewrite the last row's own values)
+          if (live) s_T[r * FIN + f] = xr[i][f];
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xr[i][f]), r0, voff + 4 * f, 0, 0);
         }
       }
@@ -1036,11 +1039,11 @@ __global__ __launch_bounds__(kXT) void k_xbasis(const int* __restrict__ rowptr,
         }
         const __amdgpu_buffer_rsrc_t rk = slab(xplanes + int64_t(k) * xpstride, sm_i);
         // (T_k is a plane of its own: no barrier between the reads of T_{k-1} and
-        // these writes; idle lanes rewrite the last row with the same values)
+        // these writes)
 #pragma unroll
         for (int f = 0; f < FIN; ++f) {
           const float o = k >= 2 ? 2.f * acc[f] - s_T[(k - 2) * MF + r * FIN + f] : acc[f];
-          s_T[k * MF + r * FIN + f] = o;
+          if (live) s_T[k * MF + r * FIN + f] = o;
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rk, voff + 4 * f, 0, 0);
         }
         __syncthreads();

@@ -506,6 +506,17 @@ def unstack_time(x: torch.Tensor, T: int) -> torch.Tensor:
     return x.reshape(N, M, C // T, T).permute(3, 0, 1, 2).contiguous()
 
 
+def dropout_seed(seed: int, rank: int, layer: int) -> int:
+    """A 64-bit mask-stream seed from (model seed, rank, layer index): a
+    splitmix64 finaliser over the three (deterministic across processes, unlike
+    Python's salted ``hash``)."""
+    z = (int(seed) * 0x9E3779B97F4A7C15 + int(rank) * 0xBF58476D1CE4E5B9 +
+         (int(layer) + 1) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & ((1 << 64) - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & ((1 << 64) - 1)
+    return z ^ (z >> 31)
+
+
 class GLSTMModel:
     """``GconvModel.inference_glstm`` (lib/gconv_lstm.py:271-281) trained as
     ``GraphModel`` trains it (lib/graph_model.py:246-310):
@@ -585,7 +596,12 @@ class GLSTMModel:
             self.W_fc = bind(w0, "conv_init/weights")
         assert off == total
         self.cells = cells
-        self.wrapped = [DropoutWrapper(c, keep_prob) if keep_prob < 1.0 else c for c in cells]
+        # each wrapper's mask stream from (model seed, rank, layer): training is
+        # reproducible from the seed, and the ranks draw independent masks for
+        # their shards (TF: one random op per wrapper per replica)
+        rank = int(getattr(comm, "rank", 0)) if comm is not None else 0
+        self.wrapped = [DropoutWrapper(c, keep_prob, seed=dropout_seed(seed, rank, li))
+                        if keep_prob < 1.0 else c for li, c in enumerate(cells)]
         # optimizer slots (TF 1.x: Adam m, v zeros; RMSProp ms ONES, mom zeros)
         self.s1 = (torch.ones if optimizer == "rmsprop" else torch.zeros)(total, **f32)
         self.s2 = torch.zeros(total, **f32)

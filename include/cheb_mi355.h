@@ -89,7 +89,10 @@ enum {
                            one launch with the recurrence in LDS where it fits
                            (default); 2: up front by one streaming launch per
                            order; 0: recomputed inside k_lstm_seq                     */
-  CG_OPT_COUNT = 8
+  CG_OPT_FAST_RPL = 8,  /* rows per lane of the fast resident forward (Fin <= 2, Fout <= 32):
+                           1: 1024 threads, one row each (default); 2: 512 threads, two rows
+                           each, the pair's sums on packed fp32                        */
+  CG_OPT_COUNT = 9
 };
 
 typedef struct cg_plan cg_plan;

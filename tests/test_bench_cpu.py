@@ -52,3 +52,13 @@ def test_committed_pmc_summary_is_config_b():
         d = json.load(fh)
     assert d["config"] == {"M": 976, "N": 256, "K": 25, "Fin": 1, "Fout": 32, "layout": "orders"}
     assert d["counters"]["cheb_bwd_fast"]["FETCH_SIZE_x2_bytes"] > 0
+
+
+def test_batch_split_weak_and_strong():
+    import argparse
+    weak = argparse.Namespace(batch=256, global_batch=None)
+    assert bench.batch_split(weak, 3, 8) == (256, 2048, False)  # config D: 2 048 over 8
+    strong = argparse.Namespace(batch=128, global_batch=512)
+    assert bench.batch_split(strong, 0, 4) == (128, 512, True)  # config E: 512 over 4
+    odd = argparse.Namespace(batch=1, global_batch=7)
+    assert [bench.batch_split(odd, r, 2)[0] for r in range(2)] == [3, 4]

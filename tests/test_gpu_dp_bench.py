@@ -97,3 +97,43 @@ def test_bench_entry_path_world2(dev):
     assert strong["scaling"] == "strong" and strong["n_gpus"] == 2
     assert strong["config"]["batch_per_gpu"] == 128 and strong["config"]["global_batch"] == 256
     assert strong["value"] > 0
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("config,batch,bucket", [("D", 2, 4 * 192 * 64), ("E", 4, 53504)])
+def test_bench_config_de_entry_world2(dev, config, batch, bucket):
+    """bench.py --config D / E (BASELINE configs[3] is an
+    8-GPU D, configs[4] a 4-GPU E) through the same N > 1 entry as config B:
+    spawn_ranks -> torchrun -> init -> barrier -> timed steps -> max over ranks
+    -> one JSON line, two ranks on this box's GPU over gloo, a reduced
+    per-rank batch (the full shapes otherwise).  Weak and strong scaling."""
+    base = ["--config", config, "--gpus", "2", "--allreduce", "torch", "--dist-backend", "gloo",
+            "--batch", str(batch), "--steps", "3", "--warmup", "1"]
+    weak = _bench_json(base)
+    assert weak["n_gpus"] == 2 and weak["steps"] == 3 and weak["warmup"] == 1
+    assert weak["scaling"] == "weak" and weak["metric"] == "Chebyshev-K fwd+bwd samples/sec"
+    c = weak["config"]
+    assert c["workload"].startswith(f"config {config}:")
+    assert c["parallelism"] == "dp2" and c["batch_per_gpu"] == batch and c["global_batch"] == 2 * batch
+    assert c["allreduce"] == "torch" and c["dist_backend"] == "gloo" and c["rccl_nranks"] is None
+    assert c["grad_bucket_bytes"] == bucket
+    assert weak["value"] > 0 and weak["ms_per_step"] > 0
+    assert abs(weak["value"] - 2 * batch * 3 / (weak["ms_per_step"] * 3 / 1e3)) < 0.01 * weak["value"]
+    r = weak["roofline"]
+    assert r["bound"] == ("hbm" if config == "D" else "mfma") and 0 < r["frac"] < 1
+    assert "cpu_baseline" not in weak
+    strong = _bench_json(base[:-6] + ["--global-batch", str(2 * batch - 1), "--steps", "2", "--warmup", "1"])
+    assert strong["scaling"] == "strong" and strong["config"]["global_batch"] == 2 * batch - 1
+    assert strong["config"]["batch_per_gpu"] == batch - 1  # rank 0's shard; rank 1 takes the remainder
+
+
+@pytest.mark.timeout(600)
+def test_bench_config_e_one_gpu_line(dev):
+    """bench.py --config E at N = 1 (the 1-rank line, with its exchange forced
+    through a 1-rank RCCL communicator: rccl_nranks == 1) and the contract
+    fields."""
+    line = _bench_json(["--config", "E", "--batch", "8", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--force-allreduce"])
+    assert line["n_gpus"] == 1 and line["config"]["rccl_nranks"] == 1
+    assert line["config"]["global_batch"] == 8 and line["config"]["parallelism"] == "dp1"
+    assert line["roofline"]["unit"] == "TFLOP/s"

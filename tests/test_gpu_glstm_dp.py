@@ -96,3 +96,39 @@ def test_glstm_model_flat_bucket_and_optimizers(dev):
     ms = 1.0 + (g * g - 1.0) * 0.1
     ref = p0 - 1e-2 * g / torch.sqrt(ms + 1e-10)
     assert O.normwise_err(res["rmsprop"][1].numpy(), ref.numpy()) < 1e-6
+
+
+def test_glstm_dropout_reproducible_from_seed(dev):
+    """keep_prob < 1 (the reference default 0.8, lib/gconv_lstm.py:616): the
+    dropout masks derive from (model seed, rank, layer), so two
+    models built with one seed train bitwise identically whatever was built
+    before them in the process, another seed (or another rank) draws other
+    masks, and the masks really drop (the step differs from keep_prob = 1)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import glstm_dp_worker as Wk
+    from cnn_graph_amd.gconv_lstm import GLSTMModel, dropout_seed
+    L, x, labels = Wk.problem()
+    xs, ys = torch.from_numpy(x[:2]).to(dev), torch.from_numpy(labels[:2]).to(dev)
+
+    class Rank:  # a comm stand-in that names a rank (world 1: no exchange)
+        def __init__(self, r):
+            self.rank, self.world = r, 1
+
+    def train(seed, keep, comm=None):
+        m = GLSTMModel(L, 2, Wk.T, Wk.FIN, num_hidden=Wk.H, K=Wk.K, out_features=Wk.FOUT,
+                       layer_count=2, keep_prob=keep, device=dev, seed=seed, comm=comm)
+        for _ in range(2):
+            m.train_step(xs, ys)
+        torch.cuda.synchronize()
+        return m.flat.cpu().clone()
+
+    a = train(7, 0.8)
+    train(9, 0.8)  # more wrappers created in between: must not shift the next model's masks
+    b = train(7, 0.8)
+    assert torch.equal(a, b)
+    assert not torch.equal(a, train(8, 0.8))
+    assert not torch.equal(a, train(7, 0.8, Rank(1)))
+    assert not torch.equal(a, train(7, 1.0))
+    assert torch.equal(a, train(7, 0.8, Rank(0)))
+    seeds = {dropout_seed(7, r, li) for r in range(8) for li in range(4)}
+    assert len(seeds) == 32 and all(0 <= s < 2 ** 64 for s in seeds)
