@@ -10,11 +10,10 @@ SRCS     := $(SRC_DIR)/cheb_fast.hip $(SRC_DIR)/cheb_resident.hip $(SRC_DIR)/che
             $(SRC_DIR)/cheb_abi.cpp $(SRC_DIR)/comm.cpp $(SRC_DIR)/coarsen.cpp \
             $(SRC_DIR)/lds_layout.cpp
 # fast resident kernels: one object per instantiation of cheb_fast_kern.h
-# (fastf_<Fin>_<Fout tiles>_<orders basis>_<rows per lane>, fastb_<Fin>_<fused dW: 1 rows, 2 orders basis>;
+# (fastf_<Fin>_<Fout tiles>_<orders basis>, fastb_<Fin>_<fused dW: 1 rows, 2 orders basis>;
 # the orders layout for Fin <= 2 only), compiled in parallel
-FAST_INST := fastf_1_1_0_1 fastf_1_2_0_1 fastf_2_1_0_1 fastf_2_2_0_1 fastf_4_1_0_1 fastf_4_2_0_1 \
-             fastf_1_1_1_1 fastf_1_2_1_1 fastf_2_1_1_1 fastf_2_2_1_1 \
-             fastf_1_1_0_2 fastf_1_1_1_2 fastf_2_1_0_2 fastf_2_1_1_2 \
+FAST_INST := fastf_1_1_0 fastf_1_2_0 fastf_2_1_0 fastf_2_2_0 fastf_4_1_0 fastf_4_2_0 \
+             fastf_1_1_1 fastf_1_2_1 fastf_2_1_1 fastf_2_2_1 \
              fastb_1_0 fastb_1_1 fastb_1_2 fastb_2_0 fastb_2_1 fastb_2_2 fastb_4_0 fastb_4_1
 OBJS     := $(patsubst $(SRC_DIR)/%,$(OBJ_DIR)/%.o,$(SRCS)) $(patsubst %,$(OBJ_DIR)/%.o,$(FAST_INST))
 DEPS     := $(OBJS:.o=.d)
@@ -30,10 +29,9 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%
 w1 = $(word 1,$(subst _, ,$*))
 w2 = $(word 2,$(subst _, ,$*))
 w3 = $(word 3,$(subst _, ,$*))
-w4 = $(word 4,$(subst _, ,$*))
 $(OBJ_DIR)/fastf_%.o: $(SRC_DIR)/cheb_fast_inst.hip
 	@mkdir -p $(OBJ_DIR)
-	$(HIPCC) $(CXXFLAGS) -DCG_FAST_FWD -DCG_FV=$(w1) -DCG_NT=$(w2) -DCG_OB=$(w3) -DCG_RPL=$(w4) -MMD -MP -c $< -o $@
+	$(HIPCC) $(CXXFLAGS) -DCG_FAST_FWD -DCG_FV=$(w1) -DCG_NT=$(w2) -DCG_OB=$(w3) -MMD -MP -c $< -o $@
 $(OBJ_DIR)/fastb_%.o: $(SRC_DIR)/cheb_fast_inst.hip
 	@mkdir -p $(OBJ_DIR)
 	$(HIPCC) $(CXXFLAGS) -DCG_FAST_BWD -DCG_FV=$(w1) -DCG_DW=$(w2) -MMD -MP -c $< -o $@

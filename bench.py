@@ -508,6 +508,7 @@ def run_config_de(args, rank, world, local, dev, json_fd):
     info.update({"batch_per_gpu": N, "global_batch": N_global, "parallelism": f"dp{world}",
                  "allreduce": (args.allreduce if comm is not None else None),
                  "dist_backend": (dist.get_backend() if world > 1 else None),
+                 "control_plane": (dist.get_backend() if world > 1 else None),
                  "rccl_nranks": rccl_nranks, "launch": "eager C-ABI calls per step"})
     out = {"metric": "Chebyshev-K fwd+bwd samples/sec", "value": round(N_global * args.steps / elapsed, 2),
            "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -564,7 +565,7 @@ def main():
                          "slower than eager launches on config B (profiles/r03_graph), so off")
     ap.add_argument("--opt", action="append", default=[],
                     help="kernel-selection option name=value (cg_set_option) for A/B runs, "
-                         "e.g. fast_rpl=2; the defaults are the measured-faster kernels")
+                         "e.g. dw_direct=0; the defaults are the measured-faster kernels")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "gloo"],
                     help="test only: gloo runs the N > 1 entry path (torchrun, init, barrier, max over "
                          "ranks) with every rank on GPU local_rank mod the visible GPUs, e.g. two "
@@ -589,7 +590,12 @@ def main():
     env_world = int(os.environ.get("WORLD_SIZE", "1"))
     if env_world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
-    rank, world, local = cdist.init("gloo" if args.dist_backend == "gloo" else None)
+    # control plane (barriers, the max over ranks, the weight broadcast, the
+    # RCCL unique id) over gloo whenever the gradient exchange is the library's
+    # own RCCL communicator (the default): a rank then holds ONE RCCL
+    # communicator, not ProcessGroupNCCL's as well
+    ctrl = "gloo" if (args.dist_backend == "gloo" or args.allreduce == "rccl") else None
+    rank, world, local = cdist.init(ctrl)
     if args.dist_backend == "gloo":
         local %= torch.cuda.device_count()
     dev = torch.device("cuda", local)
@@ -788,6 +794,7 @@ def main():
                    "parallelism": f"dp{world}",
                    "allreduce": (args.allreduce if exchange else None),
                    "dist_backend": (dist.get_backend() if world > 1 else None),
+                   "control_plane": (dist.get_backend() if world > 1 else None),
                    "rccl_nranks": rccl_nranks,
                    "options": dict(kv.split("=") for kv in args.opt) or None,
                    "launch": ("one HIP graph replay of the K captured steps" if graph is not None

@@ -24,7 +24,7 @@ __host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(
 // Kernel-selection options (cg_set_option, CG_OPT_* in include/cheb_mi355.h):
 // process-wide, read by the launch code at every launch
 enum Opt { kOptDwDirect = 0, kOptDwW2, kOptDwWaves, kOptSpmmPw, kOptGrp16, kOptGrpPc, kOptClenDy,
-           kOptSeqXpre, kOptFastRpl, kOptCount };
+           kOptSeqXpre, kOptCount };
 int option(Opt o);
 
 // Timing-ablation switches (bits 0-7 forward resident kernel, 8-15 backward,
@@ -347,13 +347,12 @@ int dw_chunks(int64_t R);
 // xb != NULL: x_fin*K more planes columns from xb (x_stride apart) and a
 // column of ones after the FinK basis columns (the gconv-LSTM's dWx and db in
 // the same pass over dy); the slabs are then [FinK + x_fin*K + 1][Fout].
-// Small dW (config A: R = N*M rows of a few columns): ONE 1024-thread block
-// forms dW = basis^T dy straight into `out` in a fixed order (no slabs, no
-// reduction launch).  dw_small_ok says whether the shape qualifies.
+// Small dW (config A: R = N*M rows of a few columns): ONE 256-thread block
+// forms dW = basis^T dy (rows layout) straight into `out` in a fixed order (no
+// slabs, no reduction launch).  dw_small_ok says whether the shape qualifies.
 bool dw_small_ok(int64_t R, int FinK, int Fout);
 hipError_t launch_dw_small(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
-                           float* out, hipStream_t s, int pl_fin = 0, int64_t pl_stride = 0,
-                           int K = 1);
+                           float* out, hipStream_t s);
 hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
                            float* slab, hipStream_t s, int pl_fin = 0, int64_t pl_stride = 0,
                            int K = 0, const float* xb = nullptr, int x_fin = 0,

@@ -1,6 +1,7 @@
 // C ABI of libcheb_mi355.so (see include/cheb_mi355.h): plan management,
 // argument validation, workspace layout and kernel-path dispatch.
 #include "../../include/cheb_mi355.h"
+#include "../../include/cheb_mi355_testing.h"
 
 #include <hip/hip_runtime.h>
 
@@ -457,14 +458,27 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
 namespace cg {
 namespace {
 // CG_OPT_* values (defaults: the measured-faster kernels) and their ranges
-std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}, {1}};
+std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}};
+// The release library accepts only the values a user would choose between;
+// the alternatives that lost every A/B exist in the ablation
+// build only (`make debug`): CG_OPT_DW_DIRECT 2 / 3 (forced direct dW), CG_OPT_DW_W2
+// 0 (one-wave dW builds), CG_OPT_SPMM_PW 0, CG_OPT_GRP_PC 0, CG_OPT_CLEN_DY 0 / 2.
 bool option_valid(int o, int v) {
+#ifndef CG_DEBUG
+  switch (o) {
+    case kOptDwDirect: return v == 0 || v == 1;
+    case kOptDwW2:
+    case kOptSpmmPw:
+    case kOptGrpPc:
+    case kOptClenDy: return v == 1;
+    default: break;
+  }
+#endif
   switch (o) {
     case kOptDwDirect: return v >= 0 && v <= 3;
     case kOptDwWaves: return v == 4 || v == 8;
     case kOptClenDy: return v >= 0 && v <= 2;
     case kOptSeqXpre: return v >= 0 && v <= 2;
-    case kOptFastRpl: return v == 1 || v == 2;
     default: return v == 0 || v == 1;
   }
 }
@@ -474,7 +488,7 @@ int option(Opt o) { return g_opts[o].load(std::memory_order_relaxed); }
 
 extern "C" {
 
-int cg_version(void) { return 201; }
+int cg_version(void) { return 300; }
 
 
 int cg_set_option(int32_t option, int32_t value) {
@@ -1035,11 +1049,9 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   if (fused) nslab_ready = N;
   // small problems (config A): dW in one block, no slabs and no reduction
   // launch (with Adam: the one result is the single slab of the fused reduction)
-  if (!nslab_ready && layout != CG_BASIS_ORDERS && cg::dw_small_ok(R, FinK, Fout) &&
+  if (!nslab_ready && layout == CG_BASIS_ROWS && cg::dw_small_ok(R, FinK, Fout) &&
       !(cg::debug_flags() & (1 << 22))) {
-    const int pl = layout == CG_BASIS_PLANES ? Fin : 0;
-    CG_HIP(cg::launch_dw_small(basis, dy, R, FinK, Fout, adam ? slabs : dW, s, pl,
-                               pl ? int64_t(R) * Fin : 0, K));
+    CG_HIP(cg::launch_dw_small(basis, dy, R, FinK, Fout, adam ? slabs : dW, s));
     if (!adam) return ok();
     nslab_ready = 1;
   }

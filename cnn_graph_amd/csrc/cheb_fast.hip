@@ -6,7 +6,7 @@
 
 namespace cg {
 namespace fastk {
-template <int FV, int NT, bool OB, int RPL>
+template <int FV, int NT, bool OB>
 hipError_t launch_fwd_fast_t(size_t lds, int N, const FastFwdArgs& a, hipStream_t s);
 template <int FV, int DW>
 hipError_t launch_bwd_fast_t(size_t lds, int N, const FastBwdArgs& a, hipStream_t s);
@@ -33,23 +33,15 @@ FastGeom fast_geometry(int M, int P, int max_row_nnz, int max_row_nnzT, int Fin,
 }
 
 hipError_t launch_fast_forward(const FastGeom& g, int N, const FastFwdArgs& a, hipStream_t s) {
-  // orders-layout basis: Fin <= 2 (cheb_abi.cpp::check_layout).  CG_OPT_FAST_RPL
-  // = 2: two rows per lane, 512 threads (Fin <= 2, one Fout tile)
-  const bool rpl2 = option(kOptFastRpl) == 2 && a.Fin <= 2 && g.nt == 1;
+  // orders-layout basis: Fin <= 2 (cheb_abi.cpp::check_layout)
 #define CG_F(FV_, NT_)                                                                   \
   if (a.Fin == FV_ && g.nt == NT_)                                                       \
-    return a.bord ? fastk::launch_fwd_fast_t<FV_, NT_, true, 1>(g.fwd_lds_ob, N, a, s)   \
-                  : fastk::launch_fwd_fast_t<FV_, NT_, false, 1>(g.fwd_lds, N, a, s);
-#define CG_F2(FV_)                                                                       \
-  if (rpl2 && a.Fin == FV_)                                                              \
-    return a.bord ? fastk::launch_fwd_fast_t<FV_, 1, true, 2>(g.fwd_lds_ob, N, a, s)     \
-                  : fastk::launch_fwd_fast_t<FV_, 1, false, 2>(g.fwd_lds, N, a, s);
-  CG_F2(1) CG_F2(2)
+    return a.bord ? fastk::launch_fwd_fast_t<FV_, NT_, true>(g.fwd_lds_ob, N, a, s)      \
+                  : fastk::launch_fwd_fast_t<FV_, NT_, false>(g.fwd_lds, N, a, s);
   CG_F(1, 1) CG_F(1, 2) CG_F(2, 1) CG_F(2, 2)
 #undef CG_F
-#undef CG_F2
-  if (a.Fin == 4 && !a.bord && g.nt == 1) return fastk::launch_fwd_fast_t<4, 1, false, 1>(g.fwd_lds, N, a, s);
-  if (a.Fin == 4 && !a.bord && g.nt == 2) return fastk::launch_fwd_fast_t<4, 2, false, 1>(g.fwd_lds, N, a, s);
+  if (a.Fin == 4 && !a.bord && g.nt == 1) return fastk::launch_fwd_fast_t<4, 1, false>(g.fwd_lds, N, a, s);
+  if (a.Fin == 4 && !a.bord && g.nt == 2) return fastk::launch_fwd_fast_t<4, 2, false>(g.fwd_lds, N, a, s);
   return hipErrorInvalidValue;
 }
 

@@ -6,11 +6,8 @@
 namespace cg {
 namespace fastk {
 #if defined(CG_FAST_FWD)
-#ifndef CG_RPL
-#define CG_RPL 1
-#endif
-template hipError_t launch_fwd_fast_t<CG_FV, CG_NT, (CG_OB != 0), CG_RPL>(size_t, int,
-                                                                         const FastFwdArgs&, hipStream_t);
+template hipError_t launch_fwd_fast_t<CG_FV, CG_NT, (CG_OB != 0)>(size_t, int, const FastFwdArgs&,
+                                                                 hipStream_t);
 #elif defined(CG_FAST_BWD)
 template hipError_t launch_bwd_fast_t<CG_FV, CG_DW>(size_t, int, const FastBwdArgs&, hipStream_t);
 #else

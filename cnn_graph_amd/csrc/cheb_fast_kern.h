@@ -133,9 +133,6 @@ __device__ __forceinline__ void setc(float4& v, int i, float x) {
 
 // Registers of the one row a thread owns.
 struct Row {
-#ifdef CG_DEBUG
-  int dbg_scalar = 0;  // ablation build: the forward's debug byte (reduce_pair)
-#endif
   int row;          // vertex, or -1 (idle)
   int rb, rb1;      // byte offsets of the row's two own records (dummy when idle)
   int rr;           // byte offset of the own-record copy read as T_{k-2}
@@ -189,51 +186,12 @@ struct Row {
 // ---------------------------------------------------------------------------
 // Forward
 // ---------------------------------------------------------------------------
-// Two rows of the same step in one lane (RPL = 2: 512 threads, 8 waves, two
-// waves per SIMD): the lane's rows are those of image threads 128w + l and
-// 128w + 64 + l, i.e. of two adjacent image waves, so the bank-aware layout's
-// 64-lane instruction groups (gathers, own-record writes) are exactly those of
-// the 1024-thread image and stay conflict-free.  FV = 1: the two rows' sums
-// run on packed fp32 (v_pk_mul_f32 / v_pk_add_f32: one rounding per product
-// and per add, as the scalar chain), half the VALU issue of two scalar chains.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int FV, int L>
-__device__ __forceinline__ void reduce_pair(const Row& r0, const Row& r1,
-                                            const typename VecT<FV>::type* g0,
-                                            const typename VecT<FV>::type* g1,
-                                            typename VecT<FV>::type& a0,
-                                            typename VecT<FV>::type& a1) {
-#pragma clang fp contract(off)
-  // (ablation build: forward bit 1 sums the two rows as two scalar chains)
-  if constexpr (FV == 1) {
-    if (CG_DBG(r0.dbg_scalar, 1)) {
-      a0 = r0.template reduce<FV, L>(g0);
-      a1 = r1.template reduce<FV, L>(g1);
-      return;
-    }
-    f32x2 a = {0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      const f32x2 v = {r0.v[j], r1.v[j]};
-      const f32x2 g = {g0[j], g1[j]};
-      a = a + v * g;
-    }
-    a0 = a.x;
-    a1 = a.y;
-  } else {
-    a0 = r0.template reduce<FV, L>(g0);
-    a1 = r1.template reduce<FV, L>(g1);
-  }
-}
-
 // OB: the basis goes out in the orders layout during the recurrence (no LDS staging)
-template <int FV, int NT, bool OB, int RPL = 1>
+template <int FV, int NT, bool OB>
 struct Fwd {
   typedef typename VecT<FV>::type V;
   static constexpr int REC = 12 * FV;
-  static constexpr int NTH = kT / RPL;   // threads of the workgroup
-  static constexpr int NW = NTH / 64;    // its waves
-  static constexpr int MT = 32 / NW;     // 32-vertex tiles per wave (ntiles <= 32)
+  static constexpr int MT = 2;  // 32-vertex tiles per wave (ntiles <= 32)
 
   const FastFwdArgs& A;
   char* ring;
@@ -243,8 +201,8 @@ struct Fwd {
   int K, M, Fout, FinK, wave, lane, li, h, ntiles, bord;
   int mb[MT];  // byte offsets of the records of this lane's MFMA tile rows
   bool keep_basis;
-  Row r[RPL];
-  V t1[RPL], t2[RPL];  // T_{k-1}, T_{k-2} of the own rows
+  Row r;
+  V t1, t2;  // T_{k-1}, T_{k-2} of the own row
   f32x16 acc[MT][NT];
 
   __device__ __forceinline__ Fwd(const FastFwdArgs& a, char* smem, int tid) : A(a) {
@@ -266,8 +224,6 @@ struct Fwd {
     bord = a.bord;
     gB = a.basis ? a.basis + size_t(blockIdx.x) * FinK * bord : nullptr;
   }
-  // image thread of this lane's row i
-  __device__ __forceinline__ int vtid(int i) const { return (wave * RPL + i) * 64 + lane; }
 
   // Contraction of the pair (T_{2s}, T_{2s+1}) on MFMA; stage the basis
   // (rows layout) or store it (orders layout: a half-wave's 32 rows of one
@@ -287,7 +243,7 @@ struct Fwd {
       }
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
-        const int tile = wave + t * NW;
+        const int tile = wave + t * kW;
         if (tile < ntiles) {
           const int m = tile * 32 + li;
           float a = 0.f;
@@ -310,32 +266,21 @@ struct Fwd {
   template <int L, int CUR, int PRV, int PRV2>
   __device__ __forceinline__ void step(int k) {
 #pragma clang fp contract(off)
-    V a[RPL];
-    if constexpr (RPL == 2) {
-      V g0[L > 0 ? L : 1], g1[L > 0 ? L : 1];
-      r[0].template gather<FV, L, PRV>(ring, g0);
-      r[1].template gather<FV, L, PRV>(ring, g1);
-      reduce_pair<FV, L>(r[0], r[1], g0, g1, a[0], a[1]);
-    } else {
-      // ablation build: 64 skips the gathers, 128 the own-record writes (LDS attribution)
-      a[0] = CG_DBG(A.dbg, 64) ? r[0].v[0] * t1[0] : r[0].template dot<FV, L, PRV>(ring);
+    // ablation build: 64 skips the gathers, 128 the own-record writes (LDS attribution)
+    const V a = CG_DBG(A.dbg, 64) ? r.v[0] * t1 : r.template dot<FV, L, PRV>(ring);
+    V o;
+    if (CG_DBG(A.dbg, 32)) {  // A/B switch: T_{k-2} of the own row re-read from the ring
+      const V p = lds_v<FV>(ring + r.rr + PRV2 * 4 * FV);
+      o = (k == 1) ? a : rec2(a, p);
+    } else {           // T_{k-2} of the own row kept in registers (this thread wrote it)
+      o = (k == 1) ? a : rec2(a, t2);
     }
-#pragma unroll
-    for (int i = 0; i < RPL; ++i) {
-      V o;
-      if (CG_DBG(A.dbg, 32)) {  // A/B switch: T_{k-2} of the own row re-read from the ring
-        const V p = lds_v<FV>(ring + r[i].rr + PRV2 * 4 * FV);
-        o = (k == 1) ? a[i] : rec2(a[i], p);
-      } else {  // T_{k-2} of the own row kept in registers (this thread wrote it)
-        o = (k == 1) ? a[i] : rec2(a[i], t2[i]);
-      }
-      if (!CG_DBG(A.dbg, 128)) {
-        lds_stv<FV>(ring + r[i].rb + CUR * 4 * FV, o);
-        lds_stv<FV>(ring + r[i].rb1 + CUR * 4 * FV, o);
-      }
-      t2[i] = t1[i];
-      t1[i] = o;
+    if (!CG_DBG(A.dbg, 128)) {
+      lds_stv<FV>(ring + r.rb + CUR * 4 * FV, o);
+      lds_stv<FV>(ring + r.rb1 + CUR * 4 * FV, o);
     }
+    t2 = t1;
+    t1 = o;
     __syncthreads();
   }
 
@@ -344,19 +289,15 @@ struct Fwd {
     constexpr int REC_ = REC;
     const int tid = threadIdx.x;
     const int n = blockIdx.x;
-#pragma unroll
-    for (int i = 0; i < RPL; ++i) r[i].template load<FV, L>(A.E, vtid(i));
-#ifdef CG_DEBUG
-    r[0].dbg_scalar = A.dbg;
-#endif
+    r.template load<FV, L>(A.E, tid);
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      const int tile = imin(wave + t * NW, ntiles - 1);
+      const int tile = imin(wave + t * kW, ntiles - 1);
       mb[t] = A.E.mpos[tile * 32 + li] * REC_;
     }
     char* smem = ring;
     if (A.ad_grad) {  // W' = ApplyAdam(W, grad), identical in every workgroup
-      for (int i = tid; i < FinK * Fout; i += NTH) {
+      for (int i = tid; i < FinK * Fout; i += kT) {
         const AdamElem e = adam_math(A.W[i], A.ad_m[i], A.ad_v[i], A.ad_grad[i], A.ad_scale,
                                      A.ad_lr_t, A.ad_b1, A.ad_b2, A.ad_eps);
         s_W[i] = e.p;
@@ -367,28 +308,25 @@ struct Fwd {
         }
       }
     } else {
-      for (int i = tid; i < FinK * Fout; i += NTH) s_W[i] = A.W ? A.W[i] : 0.f;
+      for (int i = tid; i < FinK * Fout; i += kT) s_W[i] = A.W ? A.W[i] : 0.f;
     }
     // T_0 = x into ring slot 0 ([pos][0][fin]); zero record kept at 0
     const float* xn = A.x + size_t(n) * M * FV;
-    for (int i = tid; i < M * FV; i += NTH) {
+    for (int i = tid; i < M * FV; i += kT) {
       const int m = i / FV, fin = i - m * FV;
       const float xv = xn[i];
       reinterpret_cast<float*>(smem + A.E.pos0[m] * REC_)[fin] = xv;
       reinterpret_cast<float*>(smem + A.E.pos1[m] * REC_)[fin] = xv;
     }
-    for (int i = tid; i < 32 * 3 * FV; i += NTH)  // the 32 zero records
+    for (int i = tid; i < 32 * 3 * FV; i += kT)  // the 32 zero records
       reinterpret_cast<float*>(smem + A.E.zpos * REC_)[i] = 0.f;
-    // T_0 of the own rows for the register-held T_{k-2}
+    // T_0 of the own row for the register-held T_{k-2}
+    t1 = vzero<V>();
+    if (r.row >= 0) {
 #pragma unroll
-    for (int i = 0; i < RPL; ++i) {
-      t1[i] = vzero<V>();
-      if (r[i].row >= 0) {
-#pragma unroll
-        for (int fin = 0; fin < FV; ++fin) setc(t1[i], fin, xn[r[i].row * FV + fin]);
-      }
-      t2[i] = t1[i];
+      for (int fin = 0; fin < FV; ++fin) setc(t1, fin, xn[r.row * FV + fin]);
     }
+    t2 = t1;
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -415,24 +353,20 @@ struct Fwd {
   }
 };
 
-template <int FV, int NT, bool OB, int RPL>
-__global__ __launch_bounds__(kT / RPL) void cheb_fwd_fast(FastFwdArgs A) {
+template <int FV, int NT, bool OB>
+__global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  typedef Fwd<FV, NT, OB, RPL> F;
-  constexpr int NTH = F::NTH, NW = F::NW;
+  typedef Fwd<FV, NT, OB> F;
   const int tid = threadIdx.x;
   const int n = blockIdx.x;
   CG_TS(A.ts, 0);
   F c(A, smem, tid);
   const int M = c.M, Fout = c.Fout, FinK = c.FinK;
 
-  // the whole prologue is specialised on the wave's row length (the longer of
-  // its image waves' when RPL = 2), so each thread loads exactly the L gather
-  // slots its run<L> uses
-  int wl = A.E.wlen[c.wave * RPL];
-  if (RPL == 2) wl = imin(kFastWidth, wl > A.E.wlen[c.wave * RPL + 1] ? wl : A.E.wlen[c.wave * RPL + 1]);
-  wl = __builtin_amdgcn_readfirstlane(wl);
+  // the whole prologue is specialised on the wave's row length, so each
+  // thread loads exactly the L gather slots its run<L> uses
+  const int wl = __builtin_amdgcn_readfirstlane(A.E.wlen[c.wave]);
   switch (wl) {
 #define CG_L(L_) case L_: c.template go<L_>(); break;
     CG_L(0) CG_L(1) CG_L(2) CG_L(3) CG_L(4) CG_L(5) CG_L(6) CG_L(7) CG_L(8)
@@ -449,7 +383,7 @@ __global__ __launch_bounds__(kT / RPL) void cheb_fwd_fast(FastFwdArgs A) {
     float* yn = A.y + size_t(n) * M * Fout;
 #pragma unroll
     for (int t = 0; t < F::MT; ++t) {
-      const int tile = c.wave + t * NW;
+      const int tile = c.wave + t * kW;
       if (tile < c.ntiles) {
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
@@ -478,10 +412,10 @@ __global__ __launch_bounds__(kT / RPL) void cheb_fwd_fast(FastFwdArgs A) {
       const int n4 = total >> 2;
       const float4* src = reinterpret_cast<const float4*>(c.s_B);
       float4* dst = reinterpret_cast<float4*>(basis_n);
-      for (int i = tid; i < n4; i += NTH) dst[i] = src[i];
-      for (int i = (n4 << 2) + tid; i < total; i += NTH) basis_n[i] = c.s_B[i];
+      for (int i = tid; i < n4; i += kT) dst[i] = src[i];
+      for (int i = (n4 << 2) + tid; i < total; i += kT) basis_n[i] = c.s_B[i];
     } else {
-      for (int i = tid; i < total; i += NTH) basis_n[i] = c.s_B[i];
+      for (int i = tid; i < total; i += kT) basis_n[i] = c.s_B[i];
     }
   }
   CG_TS(A.ts, 4);
@@ -841,11 +775,11 @@ hipError_t allow_big_lds(Kern k) {
                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
 }
 
-template <int FV, int NT, bool OB, int RPL>
+template <int FV, int NT, bool OB>
 hipError_t launch_fwd_fast_t(size_t lds, int N, const FastFwdArgs& a, hipStream_t s) {
-  static hipError_t attr = allow_big_lds(&cheb_fwd_fast<FV, NT, OB, RPL>);
+  static hipError_t attr = allow_big_lds(&cheb_fwd_fast<FV, NT, OB>);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((cheb_fwd_fast<FV, NT, OB, RPL>), dim3(N), dim3(kT / RPL), lds, s, a);
+  hipLaunchKernelGGL((cheb_fwd_fast<FV, NT, OB>), dim3(N), dim3(kT), lds, s, a);
   return hipGetLastError();
 }
 

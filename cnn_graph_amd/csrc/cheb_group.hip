@@ -43,9 +43,15 @@ constexpr int kGQ = 8;    // channels per group
 constexpr int kGRT = 4;   // 32-row tiles per wave (8 waves x 4 x 32 = 1024 rows)
 constexpr int kGQ16 = 16; // channels per group of the one-slot kernels (Fin % 16 == 0)
 
-// CG_OPT_SPMM_PW = 0: the resident SpMMs read their CSR metadata one entry per
-// LDS access (lds_row_spmm) instead of two (lds_row_spmm_w); A/B runs
+// CG_OPT_SPMM_PW = 0 (ablation build only): the resident SpMMs read their CSR
+// metadata one entry per LDS access (lds_row_spmm) instead of two
+// (lds_row_spmm_w); it lost every A/B (profiles/r04_pw), so the release
+// library carries only the paired form
+#ifdef CG_DEBUG
 inline bool spmm_pw() { return option(kOptSpmmPw) != 0; }
+#else
+constexpr bool spmm_pw() { return true; }
+#endif
 inline int rup(int v, int m) { return (v + m - 1) / m * m; }
 
 // block -> (sample, group): the G groups of a sample on one XCD
@@ -874,12 +880,15 @@ hipError_t launch_grp_fwd(const int* rowptr, const int* col, const float* val, c
   if (g16 && Fout <= 32) {
     static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp16_fwd<1, true>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (at != hipSuccess) return at;
+#ifdef CG_DEBUG
     static hipError_t at0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp16_fwd<1, false>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    if (at != hipSuccess) return at;
     if (at0 != hipSuccess) return at0;
-    if (spmm_pw()) hipLaunchKernelGGL((k_grp16_fwd<1, true>), dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
-    else hipLaunchKernelGGL((k_grp16_fwd<1, false>), dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+    if (!spmm_pw()) hipLaunchKernelGGL((k_grp16_fwd<1, false>), dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
+    else
+#endif
+    hipLaunchKernelGGL((k_grp16_fwd<1, true>), dim3(grp_grid(N, G)), dim3(kGT), lds, s, a);
   } else if (Fout <= 32) {
     static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_fwd<1>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
@@ -919,17 +928,21 @@ hipError_t launch_grp_clen(const int* trowptr, const int* tcol, const float* tva
   const int G = Fin / kGQ;
   GrpClenArgs a{trowptr, tcol, tval, order, M, rup(M + 1, 32), Fin, K, N, int(nnzT), G, D,
                 int64_t(N) * M * Fin, dx, dx_acc};
-  static hipError_t at0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen<false>),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   static hipError_t at1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen<true>),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-  if (at0 != hipSuccess) return at0;
   if (at1 != hipSuccess) return at1;
-  // CG_OPT_GRP_PC = 0: columns read from LDS every step (A/B; dx bitwise the same)
-  if (option(kOptGrpPc) == 0)
+#ifdef CG_DEBUG
+  // CG_OPT_GRP_PC = 0 (ablation build only): columns read from LDS every step
+  // (dx bitwise the same; lost its A/B, profiles/r04_r)
+  static hipError_t at0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_grp_clen<false>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+  if (at0 != hipSuccess) return at0;
+  if (option(kOptGrpPc) == 0) {
     hipLaunchKernelGGL(k_grp_clen<false>, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
-  else
-    hipLaunchKernelGGL(k_grp_clen<true>, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL(k_grp_clen<true>, dim3(grp_grid(N, G)), dim3(kGT), grp_clen_lds(M, nnzT), s, a);
   return hipGetLastError();
 }
 
@@ -953,7 +966,8 @@ hipError_t launch_grp_clen_dy(const int* trowptr, const int* tcol, const float* 
   if (Fin % kGQ || K < 1 || !grp_clen_dy_ok(M, nnzT, K, Fout))
     return hipErrorInvalidValue;
   const int G = Fin / kGQ;
-  const int pipe = option(kOptClenDy) == 2 ? 0 : 1;  // 2: each group's tiles up front (A/B runs)
+  // 2 (ablation build only): each group's tiles up front
+  const int pipe = option(kOptClenDy) == 2 ? 0 : 1;
   GrpClenDyArgs a{trowptr, tcol, tval, order, M, rup(M + 1, 32), Fin, K, N, int(nnzT), G, Fout,
                   Fout / 2, dy, W, dx, dx_acc, pipe, nullptr};
 #ifdef CG_DEBUG

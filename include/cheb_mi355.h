@@ -68,31 +68,32 @@ enum {
 /* Kernel-selection options for cg_set_option (process-wide, read at every
  * launch; no environment variables are read by the library).  The defaults are
  * the measured-faster choices; every alternative computes the same result
- * (bitwise, or y to fp32 rounding for CG_OPT_GRP16) and is kept as a user knob
- * for A/B measurement and as an independent cross-check in the tests. */
+ * (bitwise, or y to fp32 rounding for CG_OPT_GRP16).  Values marked [ablation
+ * build] are accepted only by the `make debug` library (the kernels behind them
+ * lost every A/B); the release library returns CG_ERR_ARG
+ * for them. */
 enum {
   CG_OPT_DW_DIRECT = 0, /* 1: k_dw_direct where a chunk has >= 256 rows and the grid fills
-                           the chip (default); 0: k_dw_slabs; 2: k_dw_direct whatever the
-                           wave count; 3: as 2 with one-float basis loads only        */
+                           the chip (default); 0: k_dw_slabs; [ablation build] 2:
+                           k_dw_direct whatever the wave count, 3: as 2 with one-float
+                           basis loads only                                           */
   CG_OPT_DW_W2 = 1,     /* 1: the two-waves-per-SIMD build of k_dw_direct where it fits
-                           (default); 0: the one-wave build                           */
+                           (default); [ablation build] 0: the one-wave build          */
   CG_OPT_DW_WAVES = 2,  /* waves per k_dw_slabs block: 8 (default) or 4               */
   CG_OPT_SPMM_PW = 3,   /* 1: resident SpMMs read CSR metadata two entries per LDS
-                           access (default); 0: one entry per access                  */
+                           access (default); [ablation build] 0: one entry per access */
   CG_OPT_GRP16 = 4,     /* 1: 16-channel group forward where it applies (default);
                            0: the 8-channel one                                       */
-  CG_OPT_GRP_PC = 5,    /* 1: k_grp_clen with register-packed columns (default); 0: LDS */
+  CG_OPT_GRP_PC = 5,    /* 1: k_grp_clen with register-packed columns (default);
+                           [ablation build] 0: columns from LDS                       */
   CG_OPT_CLEN_DY = 6,   /* 1: fused-dBasis Clenshaw k_grp_clen_dy, tiles pipelined
-                           (default); 2: each order group's tiles up front; 0: row-GEMM
-                           dBasis planes + k_grp_clen                                 */
+                           (default); [ablation build] 2: each order group's tiles up
+                           front; 0: row-GEMM dBasis planes + k_grp_clen              */
   CG_OPT_SEQ_XPRE = 7,  /* 1: the gconv-LSTM x basis of all steps formed up front,
                            one launch with the recurrence in LDS where it fits
                            (default); 2: up front by one streaming launch per
                            order; 0: recomputed inside k_lstm_seq                     */
-  CG_OPT_FAST_RPL = 8,  /* rows per lane of the fast resident forward (Fin <= 2, Fout <= 32):
-                           1: 1024 threads, one row each (default); 2: 512 threads, two rows
-                           each, the pair's sums on packed fp32                        */
-  CG_OPT_COUNT = 9
+  CG_OPT_COUNT = 8
 };
 
 typedef struct cg_plan cg_plan;
@@ -435,11 +436,8 @@ int cg_lstm_seq_forward_x(cg_plan* plan, int32_t T, int32_t N, int32_t Fin, int3
 int cg_lstm_seq_fault(cg_plan* plan, int32_t wait, int32_t clear, int32_t* fault);
 int cg_lstm_seq_status(const cg_plan* plan, int32_t N, const void* workspace, int32_t* status,
                        void* stream);
-/* Failure-detection test hook: from time step `step` on, workgroup 0 of pair 0
- * of this plan's sequence launches stops publishing its step counter, so its
- * partner times out exactly as when it is not co-resident (-1, the default:
- * off).  Plan-scoped; nothing else reads it. */
-int cg_plan_set_seq_fault_test(cg_plan* plan, int32_t step);
+/* (The failure-detection test hook cg_plan_set_seq_fault_test is declared in
+ * cheb_mi355_testing.h, not here: it is for the library's own tests.) */
 int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gates, const float* dh,
                      const float* dh_rec, const float* dc, const float* act,
                      int32_t act_unit_major, const float* c_prev, const float* c_out,

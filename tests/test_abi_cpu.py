@@ -9,16 +9,42 @@ from cnn_graph_amd import _lib
 
 
 def test_library_exports_every_header_symbol(built_lib):
+    import os
     h = _lib.lib()
-    syms = _lib.header_symbols()
-    assert len(syms) >= 19
+    public = _lib.header_symbols()
+    testing = _lib.header_symbols(os.path.join(os.path.dirname(_lib.HEADER_PATH), "cheb_mi355_testing.h"))
+    assert len(public) >= 19
+    syms = sorted(set(public) | set(testing))
     missing = [s for s in syms if not hasattr(h, s)]
     assert missing == []
-    assert set(syms) == set(_lib._SIGNATURES), "ctypes signatures out of sync with the header"
+    assert set(syms) == set(_lib._SIGNATURES), "ctypes signatures out of sync with the headers"
+    # the test-only fault hook is not part of the integration surface
+    assert "cg_plan_set_seq_fault_test" not in public and testing == ["cg_plan_set_seq_fault_test"]
 
 
 def test_version(built_lib):
-    assert _lib.lib().cg_version() == 201
+    # 0.3.0 (round 6): ablation-only option values refused, the fault hook moved
+    # to the testing header
+    assert _lib.lib().cg_version() == 300
+
+
+def test_release_library_refuses_ablation_only_options(built_lib):
+    """The kernel alternatives that lost every A/B are in the ablation build
+    only: the release library refuses their option values
+    and does not contain their kernels."""
+    h = _lib.lib()
+    for name, v in (("dw_direct", 2), ("dw_direct", 3), ("dw_w2", 0), ("spmm_pw", 0), ("grp_pc", 0),
+                    ("clen_dy", 0), ("clen_dy", 2)):
+        assert h.cg_set_option(_lib.OPTIONS[name], v) == _lib.CG_ERR_ARG, (name, v)
+    for name, v in (("dw_direct", 0), ("dw_direct", 1), ("dw_w2", 1), ("spmm_pw", 1), ("grp_pc", 1),
+                    ("clen_dy", 1)):
+        assert h.cg_set_option(_lib.OPTIONS[name], v) == _lib.CG_OK, (name, v)
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    # the one-entry-per-access grp16 forward and the LDS-columns Clenshaw kernel
+    for sym in (b"_ZN2cg12_GLOBAL__N_111k_grp16_fwdILi1ELb0EEEvNS0_10GrpFwdArgsE",
+                b"_ZN2cg12_GLOBAL__N_110k_grp_clenILb0EEEvNS0_11GrpClenArgsE"):
+        assert sym not in blob, sym
 
 
 def test_release_library_has_no_ablation_hooks(built_lib):
@@ -41,9 +67,9 @@ def test_options_roundtrip_and_validation(built_lib):
         v = _lib.get_option(name)
         assert _lib.set_option(name, v) == v
     assert _lib.get_option("dw_waves") == 8 and _lib.get_option("dw_direct") == 1
-    with _lib.options(dw_direct=0, clen_dy=2):
-        assert _lib.get_option("dw_direct") == 0 and _lib.get_option("clen_dy") == 2
-    assert _lib.get_option("dw_direct") == 1 and _lib.get_option("clen_dy") == 1
+    with _lib.options(dw_direct=0, seq_xpre=2):
+        assert _lib.get_option("dw_direct") == 0 and _lib.get_option("seq_xpre") == 2
+    assert _lib.get_option("dw_direct") == 1 and _lib.get_option("seq_xpre") == 1
     assert h.cg_set_option(99, 1) == _lib.CG_ERR_ARG
     assert h.cg_set_option(_lib.OPTIONS["dw_waves"], 5) == _lib.CG_ERR_ARG
     assert h.cg_set_option(_lib.OPTIONS["spmm_pw"], 2) == _lib.CG_ERR_ARG

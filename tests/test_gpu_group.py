@@ -103,9 +103,9 @@ def test_group_clenshaw_fused_dx_accumulate(dev):
 @pytest.mark.parametrize("gname,N,Fin,K,Fout", [("golden_E.npz", 3, 32, 20, 24), ("golden_B.npz", 2, 16, 5, 40)])
 def test_group_clenshaw_packed_columns_bitwise(dev, cg_opts, gname, N, Fin, K, Fout):
     """k_grp_clen (the dBasis-planes variant, Fout outside the fused kernel's
-    2 / 32 / 64) with the rows' columns packed in registers (default) and read
-    from LDS every step (CG_OPT_GRP_PC = 0): dx bitwise equal to each other and to
-    the steps path."""
+    2 / 32 / 64) with the rows' columns packed in registers: dx bitwise equal to
+    the steps path.  (Its LDS-columns alternative, CG_OPT_GRP_PC = 0, exists in
+    the ablation build only since round 6; the release library rejects it.)"""
     from cnn_graph_amd import ops
     from cnn_graph_amd.plan import ChebPlan
     c = case(load_golden(gname))
@@ -116,24 +116,27 @@ def test_group_clenshaw_packed_columns_bitwise(dev, cg_opts, gname, N, Fin, K, F
     Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
     dyt = _t(rng.standard_normal((N, M, Fout)), dev)
     out = {}
-    for name, variant, pc in (("pc", "auto", "1"), ("lds", "auto", "0"), ("steps", "steps", "1")):
-        cg_opts("grp_pc", pc)
+    for name, variant in (("pc", "auto"), ("steps", "steps")):
         plan = ChebPlan(Lt, device=0, path="stream", variant=variant)
         r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
         r.forward(xt, Wt)
         r.backward(dyt, Wt)
         torch.cuda.synchronize()
         out[name] = r.dx.clone()
-    assert torch.equal(out["pc"], out["lds"])
     assert torch.equal(out["pc"], out["steps"])
+    from cnn_graph_amd import _lib
+    with pytest.raises(_lib.CGError):
+        cg_opts("grp_pc", "0")
 
 
 @pytest.mark.parametrize("gname,N,Fin,K,Fout", [("golden_E.npz", 3, 32, 20, 32), ("golden_B.npz", 2, 16, 5, 32),
                                                 ("golden_B.npz", 2, 32, 7, 20)])
 def test_group_fwd_paired_metadata_bitwise(dev, cg_opts, gname, N, Fin, K, Fout):
     """k_grp16_fwd with the CSR metadata read two entries per LDS access
-    (lds_row_spmm_w, default) against one per access (CG_OPT_SPMM_PW = 0): basis
-    planes and y bitwise equal (rows start at both parities of the CSR)."""
+    (lds_row_spmm_w; rows start at both parities of the CSR) against the steps
+    path: basis planes bitwise equal, y within 1e-6 (another contraction order).
+    (The one-entry-per-access alternative, CG_OPT_SPMM_PW = 0, exists in the
+    ablation build only since round 6.)"""
     from cnn_graph_amd import ops
     from cnn_graph_amd.plan import ChebPlan
     c = case(load_golden(gname))
@@ -144,12 +147,15 @@ def test_group_fwd_paired_metadata_bitwise(dev, cg_opts, gname, N, Fin, K, Fout)
     xt = _t(rng.standard_normal((N, M, Fin)), dev)
     Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
     out = {}
-    for pw in ("1", "0"):
-        cg_opts("spmm_pw", pw)
-        plan = ChebPlan(Lt, device=0, path="stream")
+    for name, variant in (("grp", "auto"), ("steps", "steps")):
+        plan = ChebPlan(Lt, device=0, path="stream", variant=variant)
         r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="planes")
         r.forward(xt, Wt)
         torch.cuda.synchronize()
-        out[pw] = (r.basis.clone(), r.y.clone())
-    assert torch.equal(out["1"][0], out["0"][0])
-    assert torch.equal(out["1"][1], out["0"][1])
+        out[name] = (r.basis.clone(), r.y.clone())
+    assert torch.equal(out["grp"][0], out["steps"][0])
+    err = O.normwise_err(out["grp"][1].cpu().numpy(), out["steps"][1].cpu().numpy().astype(np.float64))
+    assert err < 1e-6, err
+    from cnn_graph_amd import _lib
+    with pytest.raises(_lib.CGError):
+        cg_opts("spmm_pw", "0")

@@ -244,44 +244,17 @@ def test_rccl_comm_single_rank_allreduce(dev):
     comm.close()
 
 
-@pytest.mark.parametrize("layout", ["rows", "orders"])
-@pytest.mark.parametrize("fname,fin,K,Fout,N", [("golden_B.npz", 1, 25, 32, 256), ("golden_B.npz", 2, 7, 24, 9),
-                                                ("golden_E.npz", 1, 3, 32, 5), ("golden_E.npz", 2, 12, 17, 4)])
-def test_fast_forward_two_rows_per_lane_bitwise(dev, cg_opts, layout, fname, fin, K, Fout, N):
-    """CG_OPT_FAST_RPL = 2 (cheb_fwd_fast at 512 threads, two rows per lane,
-    the pair's sums on packed fp32) against the 1 024-thread build and the
-    oracle: basis and y BITWISE the 1-row build's (same CSR-order chains, same
-    MFMA sequence per tile), basis bit-exact to the reference recurrence."""
-    from cnn_graph_amd import ops
-    c = case(load_golden(fname))
-    rng = np.random.default_rng(31 + fin + K)
-    x = rng.random((N, c["M"], fin), dtype=np.float32)
-    W = (rng.standard_normal((fin * K, Fout)) * 0.1).astype(np.float32)
-    plan = make_plan(c, "resident")
-    if layout == "orders" and plan.basis_elems(N, fin, K, Fout, "orders") is None:
-        pytest.skip("the orders layout does not apply to this shape")
-    out = {}
-    for rpl in ("1", "2"):
-        cg_opts("fast_rpl", rpl)
-        r = ops.ChebRunner(plan, N, fin, K, Fout, dev, basis_layout=layout)
-        r.forward(t(x, dev), t(W, dev))
-        torch.cuda.synchronize()
-        out[rpl] = (r.basis_rows().cpu().numpy(), r.y.cpu().numpy())
-    assert np.array_equal(out["1"][0], out["2"][0])
-    assert np.array_equal(out["1"][1], out["2"][1])
-    ob, oy = O.cheb_forward(x, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], W, K)
-    assert np.array_equal(out["2"][0], ob)
-    assert O.normwise_err(out["2"][1], oy) < TOL
-
-
 @pytest.mark.parametrize("layout,N,Fin,K,Fout,path", [("rows", 32, 1, 5, 4, "resident"),
+                                                      ("rows", 9, 2, 4, 7, "stream"),
+                                                      ("rows", 160, 1, 8, 8, "resident"),
                                                       ("rows", 9, 3, 4, 7, "stream"),
                                                       ("planes", 7, 16, 5, 4, "stream")])
 def test_small_dw_single_block(dev, layout, N, Fin, K, Fout, path):
-    """Small problems (config A's N*M = 3 200 rows x 20 outputs) form dW in ONE
-    1024-thread block straight into dW (k_dw_small: no slabs, no reduction
-    launch; profiles/r06c): within 1e-5 of float64 basis^T dy, in the rows and
-    planes basis layouts, deterministic across calls."""
+    """Small problems (config A's N*M = 3 200 rows x 20 outputs; FinK, Fout <= 8,
+    <= 16 384 rows, rows layout) form dW in ONE 256-thread block straight into
+    dW (k_dw_small: no slabs, no reduction launch; profiles/r06_A): within 1e-5
+    of float64 basis^T dy and deterministic across calls; the shapes past its
+    limits (FinK 12, the planes layout) take the slab path, same bar."""
     from cnn_graph_amd import ops
     c = case(load_golden("golden_A.npz"))
     plan = make_plan(c, path)
