@@ -351,6 +351,7 @@ int dw_chunks(int64_t R);
 // forms dW = basis^T dy (rows layout) straight into `out` in a fixed order (no
 // slabs, no reduction launch).  dw_small_ok says whether the shape qualifies.
 bool dw_small_ok(int64_t R, int FinK, int Fout);
+bool dw_small_aligned(const float* basis, const float* dy);  // both 16-byte aligned
 hipError_t launch_dw_small(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
                            float* out, hipStream_t s);
 hipError_t launch_dw_slabs(const float* basis, const float* dy, int64_t R, int FinK, int Fout,

@@ -1050,7 +1050,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
   // small problems (config A): dW in one block, no slabs and no reduction
   // launch (with Adam: the one result is the single slab of the fused reduction)
   if (!nslab_ready && layout == CG_BASIS_ROWS && cg::dw_small_ok(R, FinK, Fout) &&
-      !(cg::debug_flags() & (1 << 22))) {
+      cg::dw_small_aligned(basis, dy) && !(cg::debug_flags() & (1 << 22))) {
     CG_HIP(cg::launch_dw_small(basis, dy, R, FinK, Fout, adam ? slabs : dW, s));
     if (!adam) return ok();
     nslab_ready = 1;

@@ -951,62 +951,105 @@ __global__ __launch_bounds__(1024) void k_reduce_slabs3(const float* __restrict_
 }
 
 // dW = basis^T dy of a small problem in one block (config A: N*M = 3 200 rows,
-// FinK = 5, Fout = 4): thread t takes rows t, t + 256, .. and ALL outputs
-// (acc[j][f] in registers: a row is FinK + Fout floats, a few vector loads,
-// where an output-per-thread mapping issued one scalar load per output and row
-// and was bound by address processing, 8.6-10.7 us, profiles/r06d-e); then the
-// 256 partials of each output are summed in LDS in a fixed two-level order
-// (16 segments of 16 threads in thread order, then the segments in order), so
-// dW is bitwise reproducible (another grouping than the slabs': it agrees with
-// them to fp32 rounding).  Rows layout only (basis[r*FinK + j]): the planes
-// layout needs Fin % 16 == 0, i.e. FinK > 8.
-constexpr int kDwsT = 256, kDwsFK = 8, kDwsFO = 8;
+// FinK = 5, Fout = 4).  One CU's vector-memory pipeline is the limit of a
+// one-block kernel, so the rows reach it as whole 16-byte vectors: each chunk
+// of rows (its basis and dy spans are contiguous in the rows layout) is copied
+// into LDS with coalesced float4 loads, then thread t takes rows t, t + 512,
+// .. of the chunk from LDS and accumulates ALL outputs (acc[j][f] in
+// registers); the 512 partials of each output are summed in LDS in a fixed
+// two-level order (32 segments of 16 threads in thread order, then the
+// segments in order), so dW is bitwise reproducible (another grouping than
+// the slabs': it agrees with them to fp32 rounding).  (Per-lane scalar global
+// loads -- an output per thread, or a row per thread -- took 8.6-13 us on
+// config A, and so did this staging while each lane had one load in flight:
+// the time was memory round trips in series; profiles/r06_A.)
+// Rows layout only (basis[r*FinK + j]): the planes layout needs Fin % 16 == 0.
+constexpr int kDwsT = 512, kDwsFK = 8, kDwsFO = 8, kDwsSeg = kDwsT / 16;
+constexpr int kDwsStage = 96 * 1024;  // LDS bytes for a chunk's basis + dy spans (+ 32 B slack)
+__device__ __forceinline__ void dws_stage(const float* __restrict__ src, int64_t lo, int64_t hi,
+                                          float* dst, int64_t* base) {
+  // [lo, hi) floats of src (16-byte aligned: the host checks) into dst from the
+  // aligned floor of lo, as float4 up to the last whole vector and the <= 3
+  // trailing floats one by one (no read past hi's vector); the element at
+  // index e lands at dst[e - *base]
+  const int64_t b = lo & ~int64_t(3), e4 = hi >> 2;
+  *base = b;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  // 8 vectors per lane in flight before their LDS stores (one at a time, each
+  // load waited out its own memory round trip: ~10 us for config A's spans)
+  for (int64_t q0 = (b >> 2) + threadIdx.x; q0 < e4; q0 += 8 * kDwsT) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t q = q0 + int64_t(u) * kDwsT;
+      v[u] = s4[q < e4 ? q : e4 - 1];  // unconditional (clamped) loads
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t q = q0 + int64_t(u) * kDwsT;
+      if (q < e4) reinterpret_cast<float4*>(dst)[q - (b >> 2)] = v[u];
+    }
+  }
+  const int64_t tail = (e4 << 2) + threadIdx.x;
+  if (tail < hi && tail >= lo) dst[tail - b] = src[tail];
+}
 __global__ __launch_bounds__(kDwsT) void k_dw_small(const float* __restrict__ basis,
                                                     const float* __restrict__ dy, int64_t R,
-                                                    int FinK, int Fout, float* __restrict__ out) {
+                                                    int FinK, int Fout, int rows_per_chunk,
+                                                    float* __restrict__ out) {
 #pragma clang fp contract(off)
-  extern __shared__ float dws_sm[];
+  extern __shared__ __attribute__((aligned(16))) float dws_sm[];
   const int t = threadIdx.x;
   const int nout = FinK * Fout;
-  float* part = dws_sm;                         // [nout][kDwsT + 1]
-  float* seg = dws_sm + nout * (kDwsT + 1);     // [nout][16]
   float acc[kDwsFK][kDwsFO];
 #pragma unroll
   for (int j = 0; j < kDwsFK; ++j)
 #pragma unroll
     for (int f = 0; f < kDwsFO; ++f) acc[j][f] = 0.f;
-  for (int64_t r = t; r < R; r += kDwsT) {
-    float a[kDwsFK], b[kDwsFO];
+  float* s_a = dws_sm;
+  float* s_b = dws_sm + ((int64_t(rows_per_chunk) * FinK + 8 + 3) & ~int64_t(3));
+  for (int64_t r0 = 0; r0 < R; r0 += rows_per_chunk) {
+    const int64_t r1 = r0 + rows_per_chunk < R ? r0 + rows_per_chunk : R;
+    int64_t ba, bb;
+    dws_stage(basis, r0 * FinK, r1 * FinK, s_a, &ba);
+    dws_stage(dy, r0 * Fout, r1 * Fout, s_b, &bb);
+    __syncthreads();
+    for (int64_t r = r0 + t; r < r1; r += kDwsT) {
+      float a[kDwsFK], b[kDwsFO];
 #pragma unroll
-    for (int j = 0; j < kDwsFK; ++j) {
-      a[j] = basis[r * FinK + (j < FinK ? j : FinK - 1)];  // unconditional (clamped) loads
+      for (int j = 0; j < kDwsFK; ++j) a[j] = j < FinK ? s_a[r * FinK + j - ba] : 0.f;
+#pragma unroll
+      for (int f = 0; f < kDwsFO; ++f) b[f] = f < Fout ? s_b[r * Fout + f - bb] : 0.f;
+#pragma unroll
+      for (int j = 0; j < kDwsFK; ++j)
+#pragma unroll
+        for (int f = 0; f < kDwsFO; ++f) acc[j][f] = acc[j][f] + a[j] * b[f];
     }
-#pragma unroll
-    for (int f = 0; f < kDwsFO; ++f) b[f] = dy[r * Fout + (f < Fout ? f : Fout - 1)];
-#pragma unroll
-    for (int j = 0; j < kDwsFK; ++j)
-#pragma unroll
-      for (int f = 0; f < kDwsFO; ++f) acc[j][f] = acc[j][f] + a[j] * b[f];
+    __syncthreads();  // the chunk's spans are overwritten next
   }
+  float* part = dws_sm;                         // [nout][kDwsT + 1]
+  float* seg = dws_sm + nout * (kDwsT + 1);     // [kDwsSeg][nout]
 #pragma unroll
   for (int j = 0; j < kDwsFK; ++j)
 #pragma unroll
     for (int f = 0; f < kDwsFO; ++f)
       if (j < FinK && f < Fout) part[(j * Fout + f) * (kDwsT + 1) + t] = acc[j][f];
   __syncthreads();
-  // level 1: (output o, segment sg) sums threads 16 sg .. 16 sg + 15 in order
-  for (int e = t; e < nout * 16; e += kDwsT) {
-    const int o = e >> 4, sg = e & 15;
+  // level 1: (output o, segment sg) sums threads 16 sg .. 16 sg + 15 in order;
+  // consecutive lanes take consecutive outputs (row stride kDwsT + 1: a bank
+  // apart, so the reads are conflict-free; lanes over segments were 16-way)
+  for (int e = t; e < nout * kDwsSeg; e += kDwsT) {
+    const int sg = e / nout, o = e - sg * nout;
     float v = 0.f;
 #pragma unroll
     for (int u = 0; u < 16; ++u) v = v + part[o * (kDwsT + 1) + 16 * sg + u];
-    seg[o * 16 + sg] = v;
+    seg[sg * nout + o] = v;
   }
   __syncthreads();
   if (t < nout) {
     float v = 0.f;
 #pragma unroll
-    for (int sg = 0; sg < 16; ++sg) v = v + seg[t * 16 + sg];
+    for (int sg = 0; sg < kDwsSeg; ++sg) v = v + seg[sg * nout + t];
     out[t] = v;
   }
 }
@@ -1014,21 +1057,24 @@ __global__ __launch_bounds__(kDwsT) void k_dw_small(const float* __restrict__ ba
 }  // namespace
 
 bool dw_small_ok(int64_t R, int FinK, int Fout) {
-  return FinK >= 1 && FinK <= kDwsFK && Fout >= 1 && Fout <= kDwsFO && R >= 1 &&
-         R <= int64_t(64) * kDwsT;  // at most 64 rows per thread
+  return FinK >= 1 && FinK <= kDwsFK && Fout >= 1 && Fout <= kDwsFO && R >= 1 && R <= 16384;
+}
+bool dw_small_aligned(const float* basis, const float* dy) {
+  return ((reinterpret_cast<uintptr_t>(basis) | reinterpret_cast<uintptr_t>(dy)) & 15) == 0;
 }
 
 hipError_t launch_dw_small(const float* basis, const float* dy, int64_t R, int FinK, int Fout,
                            float* out, hipStream_t s) {
-  if (!dw_small_ok(R, FinK, Fout)) return hipErrorInvalidValue;
-  const size_t lds = size_t(FinK) * Fout * (kDwsT + 1 + 16) * 4;  // <= 64 x 273 x 4 = 70 KB
-  if (lds > size_t(64) * 1024) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_small),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       kLdsBytes);
-    if (attr != hipSuccess) return attr;
-  }
-  hipLaunchKernelGGL(k_dw_small, dim3(1), dim3(kDwsT), lds, s, basis, dy, R, FinK, Fout, out);
+  if (!dw_small_ok(R, FinK, Fout) || !dw_small_aligned(basis, dy)) return hipErrorInvalidValue;
+  // rows per chunk: both spans (+ alignment slack) within kDwsStage bytes
+  const int rpc = (kDwsStage - 64) / ((FinK + Fout) * 4);
+  const size_t red = size_t(FinK) * Fout * (kDwsT + 1 + kDwsSeg) * 4;  // <= 64 x 545 x 4 = 140 KB
+  const size_t lds = red > size_t(kDwsStage) ? red : size_t(kDwsStage);
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dw_small),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     kLdsBytes);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(k_dw_small, dim3(1), dim3(kDwsT), lds, s, basis, dy, R, FinK, Fout, rpc, out);
   return hipGetLastError();
 }
 
