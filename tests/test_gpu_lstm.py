@@ -426,6 +426,37 @@ def test_config_E_full_batch_gradients_vs_oracle(dev):
     assert int(torch.count_nonzero(xa.grad[:, rest])) == 0
 
 
+@pytest.mark.timeout(600)
+def test_config_E_every_sample_vs_oracle(dev):
+    """Config E at full size with a loss over all N = 128 samples: hs of every
+    sample and every gradient (dWx, dWh, db over the batch, dx of every
+    sample) against the float64 oracle run on the whole batch (~30 s of
+    numpy), through the one-launch layer forward and BPTT steps."""
+    from cnn_graph_amd.gconv_lstm import layer
+    Lt, _, M = graph_E()
+    T, N, Fin, H, K = 12, 128, 2, 32, 3
+    cell, L = make_cell(Lt, Fin, H, K, "reference", dev, seed=53)
+    assert cell.seq
+    g = torch.Generator(device=dev)
+    g.manual_seed(9)
+    xs = torch.rand((T, N, M, Fin), device=dev, generator=g)
+    gh = torch.randn((T, N, M, H), device=dev, generator=g)
+    xa = xs.clone().requires_grad_()
+    hs, _ = layer(cell, xa)
+    (hs * gh).sum().backward()
+    torch.cuda.synchronize()
+    f64 = lambda a: a.detach().cpu().numpy().astype(np.float64)  # noqa: E731
+    lap = oracle_lap(cell, L)
+    p = params_np(cell)
+    h_ref, _, caches = LO.layer_forward(f64(xs), p, lap, K, H)
+    assert O.normwise_err(f64(hs), h_ref) < TOL
+    dxs, _, _, dWx, dWh, db = LO.layer_backward(f64(gh), None, caches, p, lap, K, H)
+    for name, got, ref in (("dWx", cell.Wx.grad, dWx), ("dWh", cell.Wh.grad, dWh),
+                           ("db", cell.b.grad, db), ("dx", xa.grad, dxs)):
+        err = O.normwise_err(f64(got), ref)
+        assert err < TOL, (name, err)
+
+
 @pytest.mark.parametrize("Fin,K", [(2, 3), (1, 1), (8, 4), (5, 2)])
 def test_lstm_weight_grads_one_pass(dev, Fin, K):
     """cg_lstm_weight_grads (dWh, dWx and db of a layer in one pass over dpre)
