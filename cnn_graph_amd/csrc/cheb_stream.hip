@@ -888,6 +888,220 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   dw_direct_body<VA, NLA, VB, NLB, PD>(A);
 }
 
+// ---- dW on the bf16 matrix pipe, f32-accurate: k_dw_x3s ------------------
+// v_mfma_f32_32x32x16_bf16 instead of v_mfma_f32_32x32x2_f32.  Every f32
+// operand is split EXACTLY into three bf16 terms, x = hi + mid + lo (hi = the
+// top 8 significant bits by truncation, mid the next 8 of the exact remainder
+// x - hi, lo the last 8: 24 bits, the whole f32 significand), and each tile
+// accumulates the six products hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid in
+// f32 -- the dropped mid*lo, lo*mid, lo*lo are below 2^-23 of |a*b|, the size
+// of one f32 rounding.  Six bf16 MFMAs of 16 rows take 6*32 cycles against
+// 8*64 for the f32 form (2.7x the matrix rate); the split costs ~5.5 VALU
+// operations per operand element.  Sums are in a different order than
+// k_dw_slabs', so dW agrees to f32 rounding, not bitwise
+// (tests/test_gpu_dw_x3.py bounds both against float64).  (A register-only
+// form -- k_dw_direct's layout, two basis-column groups so dy was read twice
+// -- took 470 us on config E's pass against this kernel's 407-425 and was
+// dropped: profiles/r06_x3.)
+// Lane (i, h) of the MFMA holds rows 8h .. 8h+7 of a 16-row block for column
+// i of each operand (cdna_hip_programming.md, bf16 A/B lane map).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct Split3 {
+  bf16x8 hi, mid, lo;
+};
+__device__ __forceinline__ Split3 split3(const float (&v)[8]) {
+  float r[8], s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    r[j] = v[j] - __uint_as_float(__float_as_uint(v[j]) & 0xffff0000u);  // exact
+    s[j] = r[j] - __uint_as_float(__float_as_uint(r[j]) & 0xffff0000u);  // exact, <= 8 bits
+  }
+  u32x4 h, m, l;
+  // the upper halves of elements 2i (low half) and 2i+1 (high half)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    h[i] = __builtin_amdgcn_perm(__float_as_uint(v[2 * i + 1]), __float_as_uint(v[2 * i]), 0x07060302u);
+    m[i] = __builtin_amdgcn_perm(__float_as_uint(r[2 * i + 1]), __float_as_uint(r[2 * i]), 0x07060302u);
+    l[i] = __builtin_amdgcn_perm(__float_as_uint(s[2 * i + 1]), __float_as_uint(s[2 * i]), 0x07060302u);
+  }
+  Split3 x;
+  x.hi = __builtin_bit_cast(bf16x8, h);
+  x.mid = __builtin_bit_cast(bf16x8, m);
+  x.lo = __builtin_bit_cast(bf16x8, l);
+  return x;
+}
+__device__ __forceinline__ f32x16 mfma_x3(const Split3& a, const Split3& b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.mid, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.lo, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, c, 0, 0, 0);
+}
+
+// k_dw_x3s: the same split arithmetic with dy read ONCE per chunk however
+// many basis tiles there are.  One workgroup per chunk, one wave per 32-column
+// basis tile (FinK <= 256); the chunk's rows go in batches of 32: every wave
+// loads its own basis tile straight into registers, while the dy batch (NBT
+// tiles of 32 columns) is loaded once by the workgroup, split, and written to
+// LDS already in the MFMA's B-fragment layout ([piece][k-block][tile][lane]
+// x 16 B: a lane's fragment is one conflict-free ds_read_b128), double
+// buffered with one barrier per batch.  The staging is spread over every
+// thread of the workgroup: a task is one float4 (4 columns) of RPT consecutive
+// rows, i.e. RPT elements of the fragments of 4 lanes, split in registers and
+// written as RPT bf16 per piece (the barrier waits for the slowest wave, so a
+// stage done by a few waves stalls all of them).
+constexpr int kX3Rows = 32;  // rows per batch (two 16-row k-blocks)
+template <int RPT>
+__device__ __forceinline__ void x3_put(char* p, const float (&v)[RPT]) {
+  // the upper halves of v (hi terms: truncation), RPT bf16 at p (2 * RPT bytes)
+  if constexpr (RPT == 1) {
+    *reinterpret_cast<unsigned short*>(p) = static_cast<unsigned short>(__float_as_uint(v[0]) >> 16);
+  } else {
+    unsigned wv[RPT / 2];
+#pragma unroll
+    for (int i = 0; i < RPT / 2; ++i)
+      wv[i] = __builtin_amdgcn_perm(__float_as_uint(v[2 * i + 1]), __float_as_uint(v[2 * i]), 0x07060302u);
+    if constexpr (RPT == 2) {
+      *reinterpret_cast<unsigned*>(p) = wv[0];
+    } else if constexpr (RPT == 4) {
+      *reinterpret_cast<uint2*>(p) = make_uint2(wv[0], wv[1]);
+    } else {
+      *reinterpret_cast<uint4*>(p) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    }
+  }
+}
+template <int NBT, int RPT>
+__global__ __launch_bounds__(512) void k_dw_x3s(DwDirectArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int FRAG = 2 * NBT * 64;      // fragments per piece per batch (2 k-blocks)
+  constexpr int BUF = 3 * FRAG * 16;      // bytes per batch buffer
+  constexpr int NCQ = 8 * NBT;            // float4 column groups of the dy batch
+  constexpr int TASKS = (32 / RPT) * NCQ;  // (column group, RPT-row group) staging tasks
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int chunk = blockIdx.x;
+  const int64_t c0 = int64_t(chunk) * A.rpc;
+  const int64_t c1 = (c0 + A.rpc < A.R) ? c0 + A.rpc : A.R;
+  const int64_t nb = (c1 - c0 + kX3Rows - 1) / kX3Rows;
+  // this wave's basis column (tile w), VA = 1 (x planes / ones as k_dw_direct)
+  const int c = 32 * w + li;
+  const int64_t ald = A.pl_fin > 0 ? A.pl_fin : A.FinKh;
+  bool av = c < A.FinKh, aone = false;
+  const float* pa = A.basis + (av ? (A.pl_fin > 0 ? int64_t(c / A.pl_fin) * A.pl_stride + c % A.pl_fin : c) : 0) +
+                    (c0 + 8 * h) * ald;
+  int64_t lst = ald;
+  if (A.xb && !av) {
+    const int e = c - A.FinKh;
+    if (e < A.nxc) {
+      av = true;
+      pa = A.xb + int64_t(e / A.x_fin) * A.x_stride + e % A.x_fin + (c0 + 8 * h) * A.x_fin;
+      lst = A.x_fin;
+    } else if (e == A.nxc) {
+      aone = true;
+    }
+  }
+  // staging task of this thread (if any): column group cq, batch rows
+  // RPT rg .. RPT rg + RPT - 1 = k-block kr >> 4, lane half (kr >> 3) & 1,
+  // fragment elements kr & 7 ..
+  const bool stg = tid < TASKS;
+  const int cq = tid % NCQ, rg = tid / NCQ, kr = RPT * rg;
+  const bool bvq = stg && 4 * cq < A.Fout;  // Fout % 4 == 0: a group is all in or all out
+  const float* pb = A.dy + (bvq ? 4 * cq : 0) + (c0 + kr) * int64_t(A.ldd);
+  const int sfr = ((kr >> 4) * NBT + (cq >> 3)) * 64 + 4 * (cq & 7) + 32 * ((kr >> 3) & 1);
+  const int sby = 2 * (kr & 7);  // byte offset of the task's elements in a fragment
+  float ra[2][8];     // this lane's basis rows of the batch: k-block kb, element j
+  float4 rb[RPT];     // the staging task's dy rows
+  int nva[2], nvb;
+  auto fetch = [&](int64_t bi) {
+    const int64_t r0 = 32 * bi;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const int64_t left = c1 - (c0 + r0 + 16 * kb + 8 * h);
+      nva[kb] = left <= 0 ? 0 : left >= 8 ? 8 : int(left);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t ro = j < nva[kb] ? r0 + 16 * kb + j : -8 * int64_t(h);
+        ra[kb][j] = pa[ro * lst];
+      }
+    }
+    const int64_t left = c1 - (c0 + r0 + kr);
+    nvb = left <= 0 ? 0 : left >= RPT ? RPT : int(left);
+    if (stg) {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int64_t ro = j < nvb ? r0 + j : -int64_t(kr);
+        rb[j] = *reinterpret_cast<const float4*>(pb + ro * int64_t(A.ldd));
+      }
+    }
+  };
+  f32x16 acc[NBT];
+#pragma unroll
+  for (int b = 0; b < NBT; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  if (nb > 0) fetch(0);
+  for (int64_t bi = 0; bi < nb; ++bi) {
+    char* buf = smem + (bi & 1) * BUF;
+    if (stg) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float y[RPT], r[RPT], q[RPT];
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+          const float v = reinterpret_cast<const float*>(&rb[j])[e];
+          y[j] = (j < nvb && bvq) ? v : 0.f;
+          r[j] = y[j] - __uint_as_float(__float_as_uint(y[j]) & 0xffff0000u);  // exact
+          q[j] = r[j] - __uint_as_float(__float_as_uint(r[j]) & 0xffff0000u);  // exact
+        }
+        char* f = buf + (sfr + e) * 16 + sby;
+        x3_put<RPT>(f, y);
+        x3_put<RPT>(f + FRAG * 16, r);
+        x3_put<RPT>(f + 2 * FRAG * 16, q);
+      }
+    }
+    Split3 xa[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = (j < nva[kb] && av) ? ra[kb][j] : 0.f;
+        x[j] = aone ? (j < nva[kb] ? 1.f : 0.f) : v;
+      }
+      xa[kb] = split3(x);
+    }
+    __syncthreads();  // the batch's fragments are in; the other buffer is free
+    if (bi + 1 < nb) fetch(bi + 1);  // in flight during the MFMAs
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int b = 0; b < NBT; ++b) {
+        const int fr = (kb * NBT + b) * 64 + lane;
+        Split3 yb;
+        yb.hi = *reinterpret_cast<const bf16x8*>(buf + (0 * FRAG + fr) * 16);
+        yb.mid = *reinterpret_cast<const bf16x8*>(buf + (1 * FRAG + fr) * 16);
+        yb.lo = *reinterpret_cast<const bf16x8*>(buf + (2 * FRAG + fr) * 16);
+        acc[b] = mfma_x3(xa[kb], yb, acc[b]);
+      }
+  }
+  // tile (w, b): k_dw_direct's store layout
+  const int FinK = A.FinK;
+#pragma unroll
+  for (int b = 0; b < NBT; ++b) {
+    const int f = 32 * b + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int cc = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int jx = cc - A.FinKh;
+      const int jo = cc >= A.FinKh ? (jx < A.nxc ? A.FinKh + (jx % A.x_fin) * A.K + jx / A.x_fin : cc)
+                                   : A.pl_fin > 0 ? (cc % A.pl_fin) * A.K + cc / A.pl_fin : cc;
+      if (cc < FinK && f < A.Fout) A.slab[(int64_t(chunk) * FinK + jo) * A.ldd + f] = acc[b][r];
+    }
+  }
+}
+
 // out[i] = sum_z slab[z][i] in a FIXED order (bitwise reproducible): wave w of
 // a block sums the slabs z = w, w+16, ... for 64 consecutive outputs (one
 // 256-B coalesced load per slab, 8 in flight), then the 16 partial sums are
@@ -1334,6 +1548,46 @@ static bool launch_dw_direct(const float* basis, const float* dy, int64_t R, int
 #undef CG_W2
 }
 
+// k_dw_x3s (CG_OPT_DW_X3 = 1, the default) where it measured faster than the
+// f32 kernels: dy of 65-128 columns (three or four 32-column tiles, e.g. the
+// gconv-LSTM's 4H = 128 gate columns: config E's weight-gradient pass 564 ->
+// 407-425 us, profiles/r06_x3), 8 or fewer basis tiles and >= 256 chunks.
+// With one or two dy tiles the split's VALU and LDS work per MFMA is not
+// hidden and k_dw_direct stays faster (config D 2.32 vs 2.29-2.51 ms per
+// N = 32 call, config C2 0.24 vs 0.29 ms).
+static bool launch_dw_x3(const float* basis, const float* dy, int64_t R, int FinKh, int Fout,
+                         int ldd, float* slab, hipStream_t s, int pl_fin, int64_t pl_stride, int K,
+                         int chunks, int64_t rpc, const float* xb, int x_fin, int64_t x_stride,
+                         hipError_t* err) {
+  if (option(kOptDwX3) == 0 || option(kOptDwDirect) == 0 || rpc < 256 || chunks < 256) return false;
+  const int nxc = xb ? x_fin * K : 0;
+  const int FinK = FinKh + (xb ? nxc + 1 : 0);
+  const int nat = (FinK + 31) / 32, nbt = (Fout + 31) / 32;
+  const bool b16 = (reinterpret_cast<uintptr_t>(dy) & 15) == 0 && Fout % 4 == 0 && ldd % 4 == 0;
+  if (!b16 || nat > 8 || nbt < 3 || nbt > 4 || 32 * nbt > 64 * nat) return false;
+  DwDirectArgs a{basis, dy, R, rpc, chunks, 1, FinKh, Fout, ldd, slab, pl_fin, pl_stride, K,
+                 xb, x_fin > 0 ? x_fin : 1, nxc, FinK, x_stride};
+  const size_t lds = size_t(2) * 3 * 2 * nbt * 64 * 16;
+  // rows per staging task: the fewest with every task on its own thread
+  int rpt = 8;
+  while (rpt > 1 && 8 * nbt * (32 / (rpt / 2)) <= 64 * nat) rpt /= 2;
+  const void* kf = nullptr;
+#define CG_X3S(NB_)                                                                   \
+  kf = rpt == 1   ? reinterpret_cast<const void*>(&k_dw_x3s<NB_, 1>)                  \
+       : rpt == 2 ? reinterpret_cast<const void*>(&k_dw_x3s<NB_, 2>)                  \
+       : rpt == 4 ? reinterpret_cast<const void*>(&k_dw_x3s<NB_, 4>)                  \
+                  : reinterpret_cast<const void*>(&k_dw_x3s<NB_, 8>);
+  if (nbt == 3) {
+    CG_X3S(3)
+  } else {
+    CG_X3S(4)
+  }
+#undef CG_X3S
+  void* args[] = {&a};
+  *err = hipLaunchKernel(kf, dim3(unsigned(chunks)), dim3(unsigned(64 * nat)), args, lds, s);
+  return true;
+}
+
 static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int64_t R, int FinKh,
                                        int Fout, int ldd, float* slab, hipStream_t s, int pl_fin,
                                        int64_t pl_stride, int K, const float* xb, int x_fin,
@@ -1341,6 +1595,9 @@ static hipError_t launch_dw_slabs_cols(const float* basis, const float* dy, int6
   const int chunks = dw_chunks(R);
   const int64_t rpc = (R + chunks - 1) / chunks;
   hipError_t derr = hipSuccess;
+  if (launch_dw_x3(basis, dy, R, FinKh, Fout, ldd, slab, s, pl_fin, pl_stride, K, chunks, rpc, xb,
+                   x_fin, x_stride, &derr))
+    return derr;
   if (launch_dw_direct(basis, dy, R, FinKh, Fout, ldd, slab, s, pl_fin, pl_stride, K, chunks, rpc,
                        xb, x_fin, x_stride, &derr))
     return derr;

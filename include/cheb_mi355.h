@@ -93,7 +93,12 @@ enum {
                            one launch with the recurrence in LDS where it fits
                            (default); 2: up front by one streaming launch per
                            order; 0: recomputed inside k_lstm_seq                     */
-  CG_OPT_COUNT = 8
+  CG_OPT_DW_X3 = 8,     /* 1: dW GEMMs with 65-128 dy columns (the gconv-LSTM's gates)
+                           on the bf16 matrix pipe, every f32 operand split exactly
+                           into three bf16 terms, six products accumulated in f32
+                           (f32-accurate; not bitwise the f32 kernels) (default);
+                           0: the f32-MFMA kernels                                    */
+  CG_OPT_COUNT = 9
 };
 
 typedef struct cg_plan cg_plan;

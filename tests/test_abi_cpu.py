@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol(built_lib):
 def test_version(built_lib):
     # 0.3.0 (round 6): ablation-only option values refused, the fault hook moved
     # to the testing header
-    assert _lib.lib().cg_version() == 300
+    assert _lib.lib().cg_version() == 301
 
 
 def test_release_library_refuses_ablation_only_options(built_lib):
@@ -34,10 +34,10 @@ def test_release_library_refuses_ablation_only_options(built_lib):
     and does not contain their kernels."""
     h = _lib.lib()
     for name, v in (("dw_direct", 2), ("dw_direct", 3), ("dw_w2", 0), ("spmm_pw", 0), ("grp_pc", 0),
-                    ("clen_dy", 0), ("clen_dy", 2)):
+                    ("clen_dy", 0), ("clen_dy", 2), ("dw_x3", 2)):
         assert h.cg_set_option(_lib.OPTIONS[name], v) == _lib.CG_ERR_ARG, (name, v)
     for name, v in (("dw_direct", 0), ("dw_direct", 1), ("dw_w2", 1), ("spmm_pw", 1), ("grp_pc", 1),
-                    ("clen_dy", 1)):
+                    ("clen_dy", 1), ("dw_x3", 0), ("dw_x3", 1)):
         assert h.cg_set_option(_lib.OPTIONS[name], v) == _lib.CG_OK, (name, v)
     with open(_lib.LIB_PATH, "rb") as f:
         blob = f.read()

@@ -38,6 +38,7 @@ def test_dw_direct_rows_bitwise(dev, cg_opts, R, FK, Fo):
     g.manual_seed(R + FK + Fo)
     A = torch.randn((R, FK), device=dev, generator=g)
     D = torch.randn((R, Fo), device=dev, generator=g)
+    cg_opts("dw_x3", 0)  # the f32 kernels (k_dw_x3s: tests/test_gpu_dw_x3.py)
     cg_opts("dw_direct", "0")
     old = ops.weight_grad(A, D)
     cg_opts("dw_direct", "1")  # the default: k_dw_direct at this size
@@ -57,6 +58,7 @@ def test_dw_direct_planes_bitwise(dev, cg_opts, R, Fin, K, Fo):
     buf = torch.randn((K * st,), device=dev, generator=g)
     D = torch.randn((R, Fo), device=dev, generator=g)
     planes = buf[:R * Fin].view(R, Fin)
+    cg_opts("dw_x3", 0)
     cg_opts("dw_direct", "0")
     old = ops.weight_grad_planes(planes, st, K, R, D)
     cg_opts("dw_direct", "1")
@@ -81,6 +83,7 @@ def test_dw_direct_lstm_weight_grads_bitwise(dev, cg_opts, R, Fin, K):
     xbuf = torch.randn((K * xst,), device=dev, generator=g)
     dpre = torch.randn((R, 4 * H), device=dev, generator=g)
     hpl, xpl = hbuf[:R * H].view(R, H), xbuf[:R * Fin].view(R, Fin)
+    cg_opts("dw_x3", 0)
     cg_opts("dw_direct", "0")
     old = ops.lstm_weight_grads(hpl, hst, xpl, xst, K, R, dpre)
     cg_opts("dw_direct", "1")
