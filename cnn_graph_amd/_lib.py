@@ -27,7 +27,7 @@ CG_BASIS_ROWS, CG_BASIS_ORDERS, CG_BASIS_PLANES = 0, 1, 2
 BASIS_LAYOUTS = {"rows": CG_BASIS_ROWS, "orders": CG_BASIS_ORDERS, "planes": CG_BASIS_PLANES}
 # kernel-selection options (cg_set_option; include/cheb_mi355.h CG_OPT_*)
 OPTIONS = {"dw_direct": 0, "dw_w2": 1, "dw_waves": 2, "spmm_pw": 3, "grp16": 4, "grp_pc": 5,
-           "clen_dy": 6, "seq_xpre": 7, "dw_x3": 8}
+           "clen_dy": 6, "seq_xpre": 7, "dw_x3": 8, "gemm_x3": 9}
 
 
 class CGError(RuntimeError):

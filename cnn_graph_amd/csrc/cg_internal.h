@@ -24,7 +24,7 @@ __host__ __device__ inline size_t align16(size_t b) { return (b + 15) & ~size_t(
 // Kernel-selection options (cg_set_option, CG_OPT_* in include/cheb_mi355.h):
 // process-wide, read by the launch code at every launch
 enum Opt { kOptDwDirect = 0, kOptDwW2, kOptDwWaves, kOptSpmmPw, kOptGrp16, kOptGrpPc, kOptClenDy,
-           kOptSeqXpre, kOptDwX3, kOptCount };
+           kOptSeqXpre, kOptDwX3, kOptGemmX3, kOptCount };
 int option(Opt o);
 
 // Timing-ablation switches (bits 0-7 forward resident kernel, 8-15 backward,

@@ -458,7 +458,7 @@ int workspace_bytes(const cg_plan* p, int32_t N, int32_t Fin, int32_t K, int32_t
 namespace cg {
 namespace {
 // CG_OPT_* values (defaults: the measured-faster kernels) and their ranges
-std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}, {1}};
+std::atomic<int> g_opts[kOptCount] = {{1}, {1}, {8}, {1}, {1}, {1}, {1}, {1}, {1}, {1}};
 // The release library accepts only the values a user would choose between;
 // the alternatives that lost every A/B exist in the ablation
 // build only (`make debug`): CG_OPT_DW_DIRECT 2 / 3 (forced direct dW), CG_OPT_DW_W2

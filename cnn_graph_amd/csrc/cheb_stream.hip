@@ -422,6 +422,117 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
   }
 }
 
+// ---- the skinny row GEMM on the bf16 matrix pipe, f32-accurate ----------------
+// k_rowgemm's job (same arguments, same persistent 128-row tiles, same
+// epilogue) with every f32 operand split exactly into three bf16 terms and six
+// v_mfma_f32_32x32x16_bf16 per 16-deep k-block (split3 / mfma_x3 below: 2.7x
+// the f32 matrix rate at f32 accuracy).  B_p is split ONCE per block into LDS
+// in the B-fragment layout [k-block][tile][term][lane] x 16 B (lane (i, h)
+// holds B[16 kb + 8h + j][32 t + i], j = 0..7: one ds_read_b128 per fragment);
+// lane (i, h) of a wave streams A[r0 + i][16 kb + 8h .. + 7] -- 32 contiguous
+// bytes -- from HBM, one k-block ahead of its MFMAs, and splits it in registers.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct Split3 {
+  bf16x8 hi, mid, lo;
+};
+__device__ __forceinline__ Split3 split3(const float (&v)[8]);
+__device__ __forceinline__ f32x16 mfma_x3(const Split3& a, const Split3& b, f32x16 c);
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_rowgemm_x3(RowGemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char Bx[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int p = blockIdx.y;
+  const int KB = (a.Kc + 15) / 16;
+  bf16x8* bf = reinterpret_cast<bf16x8*>(Bx);
+  for (int e = tid; e < KB * NT * 64; e += 256) {
+    const int l = e & 63, t = (e >> 6) % NT, kb = (e >> 6) / NT;
+    const int j = t * 32 + (l & 31);
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int kk = kb * 16 + 8 * (l >> 5) + q;
+      const int k = a.apl_fin > 0 ? (kk % a.apl_fin) * a.bmapK + kk / a.apl_fin : kk;
+      float x = 0.f;
+      if (kk < a.Kc && j < a.Nc) {
+        const int pp = a.pfin > 0 ? j / a.pfin : p;
+        const int jj = a.pfin > 0 ? j - pp * a.pfin : j;
+        x = a.B[pp * a.bs_p + int64_t(k) * a.bs_k + int64_t(jj) * a.bs_j];
+      }
+      v[q] = x;
+    }
+    const Split3 sp = split3(v);
+    bf16x8* d = bf + ((kb * NT + t) * 3) * 64 + l;
+    d[0] = sp.hi;
+    d[64] = sp.mid;
+    d[128] = sp.lo;
+  }
+  __syncthreads();
+  float* C = a.C + p * a.c_plane;
+  const int64_t ntiles = (a.R + 127) / 128;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * 128 + wave * 32;
+    if (r0 >= a.R) continue;
+    const int64_t row = (r0 + i < a.R) ? r0 + i : a.R - 1;
+    const float* arow = a.A + row * (a.apl_fin > 0 ? a.apl_fin : a.lda);
+    // elements 16 kb + 8h .. + 7 of this row (planes layout: apl_fin % 16 == 0,
+    // so the eight sit in one plane)
+    auto ld = [&](float (&v)[8], int kb) {
+      const int k0 = kb * 16 + 8 * h;
+      const float* ap = a.apl_fin > 0 ? arow + (k0 / a.apl_fin) * a.apl_stride + k0 % a.apl_fin : arow + k0;
+      if (a.vecA && k0 + 8 <= a.Kc) {
+        const float4 x0 = *reinterpret_cast<const float4*>(ap);
+        const float4 x1 = *reinterpret_cast<const float4*>(ap + 4);
+        v[0] = x0.x, v[1] = x0.y, v[2] = x0.z, v[3] = x0.w;
+        v[4] = x1.x, v[5] = x1.y, v[6] = x1.z, v[7] = x1.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = k0 + q < a.Kc ? ap[q] : 0.f;
+      }
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[t][q] = 0.f;
+    float va[8];
+    ld(va, 0);
+    for (int kb = 0; kb < KB; ++kb) {
+      const Split3 xa = split3(va);
+      if (kb + 1 < KB) ld(va, kb + 1);  // the next k-block in flight during the MFMAs
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const bf16x8* f = bf + ((kb * NT + t) * 3) * 64 + lane;
+        Split3 yb;
+        yb.hi = f[0];
+        yb.mid = f[64];
+        yb.lo = f[128];
+        acc[t] = mfma_x3(xa, yb, acc[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int jcol = t * 32 + i;
+      if (jcol >= a.Nc) continue;
+      const int pp = a.pfin > 0 ? jcol / a.pfin : 0;
+      const int col = a.pfin > 0 ? jcol - pp * a.pfin : jcol;
+      float* Cp = C + pp * a.c_plane;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t rr = r0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (rr < a.R) {
+          float v = acc[t][q];
+          if (a.res) v = v + a.res[rr * a.ldc + col];
+          if (a.act) v = v > 0.f ? v : 0.f;
+          Cp[rr * a.ldc + col] = v;
+        }
+      }
+    }
+  }
+}
+
 // Reverse (Clenshaw) step over L~^T in the sample-major layout:
 //   G_k = D_k + c * (L~^T G_{k+1}) - G_{k+2},  c = 2 (k >= 1) or 1 (k = 0),
 // D_k = plane k of dBasis in the k-major layout [K][N][M][Fin] (written so by
@@ -905,11 +1016,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // dropped: profiles/r06_x3.)
 // Lane (i, h) of the MFMA holds rows 8h .. 8h+7 of a 16-row block for column
 // i of each operand (cdna_hip_programming.md, bf16 A/B lane map).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-struct Split3 {
-  bf16x8 hi, mid, lo;
-};
+// (bf16x8, Split3: declared with k_rowgemm_x3 above)
 __device__ __forceinline__ Split3 split3(const float (&v)[8]) {
   float r[8], s[8];
 #pragma unroll
@@ -1363,8 +1470,33 @@ hipError_t launch_rowgemm(const float* A, int64_t R, int Kc, int lda, const floa
                 int(arow_elems % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0),
                 apl_fin, apl_stride, bmapK};
   const int NT = (Nc + 31) / 32;
-  const size_t lds = size_t(2) * a.KC2 * NT * 32 * 4;
   const int64_t ntiles = (R + 127) / 128;
+  if (option(kOptGemmX3) != 0 && NT <= 8) {
+    // the split-bf16 form: B_p's three terms in LDS, [k-block][tile][term][lane] x 16 B
+    const size_t lx = size_t((Kc + 15) / 16) * NT * 3 * 64 * 16;
+    if (lx <= size_t(kLdsBytes)) {
+      const void* k = nullptr;
+      switch (NT) {
+#define CG_RGX(n) \
+  case n: k = reinterpret_cast<const void*>(&k_rowgemm_x3<n>); break;
+        CG_RGX(1) CG_RGX(2) CG_RGX(3) CG_RGX(4) CG_RGX(5) CG_RGX(6) CG_RGX(7) default: CG_RGX(8)
+#undef CG_RGX
+      }
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      static ResidentCache xcache;
+      const int res_blocks = xcache.get(dev, k, 256, lx, [&](const void* kf, int thr, size_t l, int* per_cu,
+                                                             int* cus) {
+        (void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kf, thr, l) == hipSuccess &&
+               hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
+      });
+      const dim3 grid(persistent_grid(ntiles, res_blocks, planes), unsigned(planes)), block(256);
+      void* args[] = {&a};
+      return hipLaunchKernel(k, grid, block, args, lx, s);
+    }
+  }
+  const size_t lds = size_t(2) * a.KC2 * NT * 32 * 4;
   // every chunk 16 contiguous in-range floats, at least 3 of them per half
   const bool pf = a.vecA && a.KC2 % 16 == 0 && 2 * a.KC2 <= Kc && a.KC2 / 16 >= 3;
   // the persistent blocks: as many as are resident at once (a grid beyond that

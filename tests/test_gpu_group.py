@@ -43,7 +43,11 @@ CASES = [("golden_E.npz", 3, 32, 20, 32), ("golden_E.npz", 2, 16, 7, 64),
 
 
 @pytest.mark.parametrize("gname,N,Fin,K,Fout", CASES)
-def test_group_clenshaw_fused_dbasis(dev, gname, N, Fin, K, Fout):
+def test_group_clenshaw_fused_dbasis(dev, cg_opts, gname, N, Fin, K, Fout):
+    """The fused-dBasis group Clenshaw (auto) against the steps path: dx
+    bitwise equal when the steps path's dBasis GEMM is the f32-MFMA k_rowgemm
+    (CG_OPT_GEMM_X3 = 0: same products, same order); with the default
+    split-bf16 row GEMM the steps path's dx / dW within 1e-5 of float64."""
     from cnn_graph_amd import ops
     from cnn_graph_amd.plan import ChebPlan
     c = case(load_golden(gname))
@@ -55,8 +59,9 @@ def test_group_clenshaw_fused_dbasis(dev, gname, N, Fin, K, Fout):
     dy = rng.standard_normal((N, M, Fout)).astype(np.float32)
     xt, Wt, dyt = _t(x, dev), _t(W, dev), _t(dy, dev)
     out = {}
-    for variant in ("auto", "steps"):
-        plan = ChebPlan(Lt, device=0, path="stream", variant=variant)
+    for variant, x3 in (("auto", 0), ("steps", 0), ("steps_x3", 1)):
+        cg_opts("gemm_x3", x3)
+        plan = ChebPlan(Lt, device=0, path="stream", variant=variant.split("_")[0])
         r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout="rows")
         r.forward(xt, Wt)
         r.backward(dyt, Wt)
@@ -66,8 +71,9 @@ def test_group_clenshaw_fused_dbasis(dev, gname, N, Fin, K, Fout):
     assert torch.equal(out["auto"][1], out["steps"][1]), "dx differs from the steps path"
     basis = out["auto"][0].cpu().numpy()
     odx, odW = O.cheb_backward(dy, basis, W, c["Lt_rowptr"], c["Lt_col"], c["Lt_val"], N, M, Fin, K)
-    assert O.normwise_err(out["auto"][1].cpu().numpy(), odx) < TOL
-    assert O.normwise_err(out["auto"][2].cpu().numpy(), odW) < TOL
+    for v in ("auto", "steps_x3"):
+        assert O.normwise_err(out[v][1].cpu().numpy(), odx) < TOL
+        assert O.normwise_err(out[v][2].cpu().numpy(), odW) < TOL
 
 
 def test_group_clenshaw_fused_dx_accumulate(dev):
@@ -144,6 +150,7 @@ def test_group_fwd_paired_metadata_bitwise(dev, cg_opts, gname, N, Fin, K, Fout)
     Lt = scipy.sparse.csr_matrix((c["Lt_val"], c["Lt_col"], c["Lt_rowptr"]), shape=(M, M))
     assert (np.asarray(c["Lt_rowptr"][:-1]) % 2 == 1).any()
     rng = np.random.default_rng(N + Fin + K + Fout + 11)
+    cg_opts("gemm_x3", 0)  # the steps path's y on the f32-MFMA row GEMM
     xt = _t(rng.standard_normal((N, M, Fin)), dev)
     Wt = _t(rng.standard_normal((Fin * K, Fout)) * 0.1, dev)
     out = {}

@@ -351,3 +351,34 @@ def _f64_cheb_chunks(rp, ci, v, M, x, W, dy, K, dev, chunk=2):
             b1, b2 = dB[k] + 2.0 * ltmul(b1) - b2, b1
         dx64 = dB[0] + ltmul(b1) - b2
         yield c, y64, dx64.view(M, nc, Fin).permute(1, 0, 2), dW.view(Fin * K, Fout)
+
+
+@pytest.mark.parametrize("which", ["C", "D"])
+def test_gemm_x3_streaming_vs_oracle(dev, cg_opts, graph_c, graph_d, which):
+    """CG_OPT_GEMM_X3 = 1: the streaming path's row GEMMs (y = basis W, dBasis
+    = dy W^T) on the split-bf16 matrix pipe: basis still bit-exact, y / dx / dW
+    within 1e-5 of the float64 oracle (config C at its Fin = 32 layer-2 shape,
+    N = 4; config D one sample, Fin = Fout = 64, K = 3)."""
+    from cnn_graph_amd import ops
+    if which == "C":
+        rp, ci, v, M = graph_c["Lt_rowptr"], graph_c["Lt_col"], graph_c["Lt_val"], graph_c["M"]
+        N, Fin, K, Fout = 4, 32, 5, 32
+    else:
+        rp, ci, v, M = graph_d
+        N, Fin, K, Fout = 1, 64, 3, 64
+    rng = np.random.default_rng(23)
+    x = rng.random((N, M, Fin), dtype=np.float32)
+    W = (rng.standard_normal((Fin * K, Fout)) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((N, M, Fout)).astype(np.float32)
+    plan = plan_of(rp, ci, v, M)
+    assert plan.query_path(N, Fin, K, Fout) == "stream"
+    cg_opts("gemm_x3", 1)
+    basis, y = ops.cheb_forward(plan, t(x, dev), t(W, dev), K)
+    dx, dW = ops.cheb_backward(plan, t(dy, dev), basis, t(W, dev), K)
+    torch.cuda.synchronize()
+    ob, oy = O.cheb_forward(x, rp, ci, v, W, K)
+    assert np.array_equal(basis.cpu().numpy().reshape(ob.shape), ob)
+    assert O.normwise_err(y.cpu().numpy(), oy) < TOL
+    odx, odW = O.cheb_backward(dy, ob, W, rp, ci, v, N, M, Fin, K)
+    assert O.normwise_err(dx.cpu().numpy(), odx) < TOL
+    assert O.normwise_err(dW.cpu().numpy(), odW) < TOL
