@@ -422,7 +422,7 @@ hipError_t launch_lstm_hstep(int gates, int N, int M, int K, const int* rowptr, 
 // xfin: feat_in of a fused x-conv (0: gx precomputed)
 size_t lstm_seq_lds(int M, int K, int64_t nnz, int xfin);
 bool lstm_seq_ok(int M, int H, int K, int64_t nnz, int xfin = 0);
-size_t lstm_bstep_lds(int M, int K, int64_t nnzT);
+size_t lstm_bstep_lds(int M, int K, int64_t nnzT, bool x3);
 bool lstm_bstep_ok(int M, int H, int K, int64_t nnzT);
 // workgroup pairs of the persistent forward (min(N, CUs / 2))
 int lstm_seq_pairs(int N, int device);

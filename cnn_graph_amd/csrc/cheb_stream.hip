@@ -22,6 +22,7 @@
 // the basis is bit-identical to the resident path and to lib/graph.py::chebyshev.
 #include "cg_internal.h"
 #include "occupancy_cache.h"
+#include "split_bf16.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -431,13 +432,9 @@ __global__ __launch_bounds__(256) void k_rowgemm(RowGemmArgs a) {
 // holds B[16 kb + 8h + j][32 t + i], j = 0..7: one ds_read_b128 per fragment);
 // lane (i, h) of a wave streams A[r0 + i][16 kb + 8h .. + 7] -- 32 contiguous
 // bytes -- from HBM, one k-block ahead of its MFMAs, and splits it in registers.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-struct Split3 {
-  bf16x8 hi, mid, lo;
-};
-__device__ __forceinline__ Split3 split3(const float (&v)[8]);
-__device__ __forceinline__ f32x16 mfma_x3(const Split3& a, const Split3& b, f32x16 c);
+using x3::bf16x8;
+using x3::Split3;
+using x3::split3;
 
 template <int NT>
 __global__ __launch_bounds__(256) void k_rowgemm_x3(RowGemmArgs a) {
@@ -509,7 +506,7 @@ __global__ __launch_bounds__(256) void k_rowgemm_x3(RowGemmArgs a) {
         yb.hi = f[0];
         yb.mid = f[64];
         yb.lo = f[128];
-        acc[t] = mfma_x3(xa, yb, acc[t]);
+        acc[t] = x3::mfma32_x3(xa, yb, acc[t]);
       }
     }
 #pragma unroll
@@ -1000,54 +997,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // ---- dW on the bf16 matrix pipe, f32-accurate: k_dw_x3s ------------------
-// v_mfma_f32_32x32x16_bf16 instead of v_mfma_f32_32x32x2_f32.  Every f32
-// operand is split EXACTLY into three bf16 terms, x = hi + mid + lo (hi = the
-// top 8 significant bits by truncation, mid the next 8 of the exact remainder
-// x - hi, lo the last 8: 24 bits, the whole f32 significand), and each tile
-// accumulates the six products hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid in
-// f32 -- the dropped mid*lo, lo*mid, lo*lo are below 2^-23 of |a*b|, the size
-// of one f32 rounding.  Six bf16 MFMAs of 16 rows take 6*32 cycles against
-// 8*64 for the f32 form (2.7x the matrix rate); the split costs ~5.5 VALU
-// operations per operand element.  Sums are in a different order than
-// k_dw_slabs', so dW agrees to f32 rounding, not bitwise
+// The split arithmetic of split_bf16.h on v_mfma_f32_32x32x16_bf16.  Sums run
+// in another order than k_dw_slabs', so dW agrees to f32 rounding, not bitwise
 // (tests/test_gpu_dw_x3.py bounds both against float64).  (A register-only
 // form -- k_dw_direct's layout, two basis-column groups so dy was read twice
 // -- took 470 us on config E's pass against this kernel's 407-425 and was
-// dropped: profiles/r06_x3.)
-// Lane (i, h) of the MFMA holds rows 8h .. 8h+7 of a 16-row block for column
-// i of each operand (cdna_hip_programming.md, bf16 A/B lane map).
-// (bf16x8, Split3: declared with k_rowgemm_x3 above)
-__device__ __forceinline__ Split3 split3(const float (&v)[8]) {
-  float r[8], s[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    r[j] = v[j] - __uint_as_float(__float_as_uint(v[j]) & 0xffff0000u);  // exact
-    s[j] = r[j] - __uint_as_float(__float_as_uint(r[j]) & 0xffff0000u);  // exact, <= 8 bits
-  }
-  u32x4 h, m, l;
-  // the upper halves of elements 2i (low half) and 2i+1 (high half)
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    h[i] = __builtin_amdgcn_perm(__float_as_uint(v[2 * i + 1]), __float_as_uint(v[2 * i]), 0x07060302u);
-    m[i] = __builtin_amdgcn_perm(__float_as_uint(r[2 * i + 1]), __float_as_uint(r[2 * i]), 0x07060302u);
-    l[i] = __builtin_amdgcn_perm(__float_as_uint(s[2 * i + 1]), __float_as_uint(s[2 * i]), 0x07060302u);
-  }
-  Split3 x;
-  x.hi = __builtin_bit_cast(bf16x8, h);
-  x.mid = __builtin_bit_cast(bf16x8, m);
-  x.lo = __builtin_bit_cast(bf16x8, l);
-  return x;
-}
-__device__ __forceinline__ f32x16 mfma_x3(const Split3& a, const Split3& b, f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.mid, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, b.hi, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.lo, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, b.hi, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.mid, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, c, 0, 0, 0);
-}
-
-// k_dw_x3s: the same split arithmetic with dy read ONCE per chunk however
+// dropped: profiles/r06_x3.)  Lane (i, h) of the MFMA holds rows 8h .. 8h+7 of
+// a 16-row block for column i of each operand (the bf16 A/B lane map).
+// k_dw_x3s: dy read ONCE per chunk however
 // many basis tiles there are.  One workgroup per chunk, one wave per 32-column
 // basis tile (FinK <= 256); the chunk's rows go in batches of 32: every wave
 // loads its own basis tile straight into registers, while the dy batch (NBT
@@ -1190,7 +1147,7 @@ __global__ __launch_bounds__(512) void k_dw_x3s(DwDirectArgs A) {
         yb.hi = *reinterpret_cast<const bf16x8*>(buf + (0 * FRAG + fr) * 16);
         yb.mid = *reinterpret_cast<const bf16x8*>(buf + (1 * FRAG + fr) * 16);
         yb.lo = *reinterpret_cast<const bf16x8*>(buf + (2 * FRAG + fr) * 16);
-        acc[b] = mfma_x3(xa[kb], yb, acc[b]);
+        acc[b] = x3::mfma32_x3(xa[kb], yb, acc[b]);
       }
   }
   // tile (w, b): k_dw_direct's store layout

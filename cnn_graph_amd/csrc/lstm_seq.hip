@@ -56,6 +56,7 @@
 //   units.  The h-weight gradient is summed afterwards per Chebyshev order
 //   over all steps from the forward's planes (one GEMM per order).
 #include "cg_internal.h"
+#include "split_bf16.h"
 #include "lds_spmm.h"
 #include "lstm_gates.h"
 
@@ -710,7 +711,12 @@ struct BStepArgs {
   unsigned long long* ts;  // ablation build: phase stamps (CG_TS), else NULL
 };
 
-template <int K>
+// X3: D_k = dpre Wh_k^T on v_mfma_f32_16x16x32_bf16 with the exact three-term
+// split of split_bf16.h (2.7x the f32 matrix rate, f32-accurate; Wh_k's terms
+// staged once in LDS as A fragments [k][gate block 4][term 3][lane 64] x 16 B:
+// lane (i, q) holds Wh_k[16u + i][32 kb + 8q + j]); the lane's dpre of gate kb,
+// units 8q .. 8q+7, is exactly its B fragment of k-block kb.
+template <int K, bool X3>
 __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -728,8 +734,8 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     u = blockIdx.x & 1;
   }
   float* slot = smem;                // [Mr][16] G_{k+1} (row M: zeros)
-  float* s_W = slot + A.Mr * kBS;   // [K][s 32][q 4][i 16]
-  float* s_val = s_W + K * 2048;
+  float* s_W = slot + A.Mr * kBS;   // [K][s 32][q 4][i 16] (X3: fragments, above)
+  float* s_val = s_W + K * (X3 ? 3072 : 2048);
   unsigned short* s_col = reinterpret_cast<unsigned short*>(s_val + A.nnz);
   // A operand of MFMA step s, order o: lane (i, q) holds Wh[(16u + i) K + o][g]
   // with g the gate column (s % 4) * 32 + 8q + s / 4 -- the column whose dpre
@@ -745,14 +751,27 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     const int idx = wave * 128 + rt * 16 + jr;
     rows[rt] = idx < M ? A.order[idx] : M;
   }
-  constexpr int kWq = K * 2048 / kST, kCsr1 = 16;
+  constexpr int kWq = X3 ? 1 : K * 2048 / kST, kCsr1 = 16;
+  constexpr int kWf = X3 ? (K * 256 + kST - 1) / kST : 1;  // X3: fragments per thread
   float wv[kWq], cv[kCsr1];
+  float4 wf[kWf][2];
   int cc[kCsr1];
+  if constexpr (X3) {
 #pragma unroll
-  for (int qd = 0; qd < kWq; ++qd) {
-    const int e = tid + qd * kST;
-    const int i = e & 15, qq = (e >> 4) & 3, s = (e >> 6) & 31, o = e >> 11;
-    wv[qd] = A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
+    for (int qd = 0; qd < kWf; ++qd) {
+      const int e = tid + qd * kST;  // fragment (o, kb, lane l)
+      const int l = e & 63, kb = (e >> 6) & 3, o = e >> 8;
+      const float* src = A.Wh + int64_t((16 * u + (l & 15)) * K + (o < K ? o : 0)) * 128 + kb * 32 + 8 * (l >> 4);
+      wf[qd][0] = *reinterpret_cast<const float4*>(src);
+      wf[qd][1] = *reinterpret_cast<const float4*>(src + 4);
+    }
+  } else {
+#pragma unroll
+    for (int qd = 0; qd < kWq; ++qd) {
+      const int e = tid + qd * kST;
+      const int i = e & 15, qq = (e >> 4) & 3, s = (e >> 6) & 31, o = e >> 11;
+      wv[qd] = A.Wh[int64_t((16 * u + i) * K + o) * 128 + (s & 3) * 32 + 8 * qq + (s >> 2)];
+    }
   }
 #pragma unroll
   for (int qd = 0; qd < kCsr1; ++qd) {
@@ -765,8 +784,25 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
     rb[rt] = rows[rt] < M ? A.trowptr[rows[rt]] : 0;
     re[rt] = rows[rt] < M ? A.trowptr[rows[rt] + 1] : 0;
   }
+  if constexpr (X3) {
+    x3::bf16x8* fw = reinterpret_cast<x3::bf16x8*>(s_W);
 #pragma unroll
-  for (int qd = 0; qd < kWq; ++qd) s_W[tid + qd * kST] = wv[qd];
+    for (int qd = 0; qd < kWf; ++qd) {
+      const int e = tid + qd * kST;
+      if (e < K * 256) {
+        const float v[8] = {wf[qd][0].x, wf[qd][0].y, wf[qd][0].z, wf[qd][0].w,
+                            wf[qd][1].x, wf[qd][1].y, wf[qd][1].z, wf[qd][1].w};
+        const x3::Split3 sp = x3::split3(v);
+        x3::bf16x8* d = fw + ((e >> 6) * 3) * 64 + (e & 63);  // (o * 4 + kb) * 3 terms
+        d[0] = sp.hi;
+        d[64] = sp.mid;
+        d[128] = sp.lo;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int qd = 0; qd < kWq; ++qd) s_W[tid + qd * kST] = wv[qd];
+  }
 #pragma unroll
   for (int qd = 0; qd < kCsr1; ++qd) {
     const int e = tid + qd * kST;
@@ -873,13 +909,30 @@ __global__ __launch_bounds__(kST) void k_lstm_bstep(BStepArgs A) {
         for (int m = 0; m < 8; ++m) dp[g][m] = 0.f;
     }
     // D_o^T[channel 16u + i][row] += Wh_o[.][g] dpre[row][g]
+    if constexpr (X3) {
+      const x3::bf16x8* fw = reinterpret_cast<const x3::bf16x8*>(s_W) + lane;
 #pragma unroll
-    for (int o = 0; o < K && !CG_DBG(A.dbg, 1); ++o) {
-      const float* wo = s_W + o * 2048 + lane;
+      for (int kb = 0; kb < 4 && !CG_DBG(A.dbg, 1); ++kb) {
+        const x3::Split3 b = x3::split3(dp[kb]);
 #pragma unroll
-      for (int s = 0; s < 32; ++s)
-        acc[rt][o] = __builtin_amdgcn_mfma_f32_16x16x4f32(wo[s * 64], dp[s & 3][s >> 2], acc[rt][o],
-                                                          0, 0, 0);
+        for (int o = 0; o < K; ++o) {
+          const x3::bf16x8* f = fw + ((o * 4 + kb) * 3) * 64;
+          x3::Split3 w;
+          w.hi = f[0];
+          w.mid = f[64];
+          w.lo = f[128];
+          acc[rt][o] = x3::mfma16_x3(w, b, acc[rt][o]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < K && !CG_DBG(A.dbg, 1); ++o) {
+        const float* wo = s_W + o * 2048 + lane;
+#pragma unroll
+        for (int s = 0; s < 32; ++s)
+          acc[rt][o] = __builtin_amdgcn_mfma_f32_16x16x4f32(wo[s * 64], dp[s & 3][s >> 2], acc[rt][o],
+                                                            0, 0, 0);
+      }
     }
   }
   CG_TS(A.ts, 2);
@@ -1067,14 +1120,14 @@ bool lstm_seq_ok(int M, int H, int K, int64_t nnz, int xfin) {
          lstm_seq_lds(M, K, nnz, xfin) <= size_t(kLdsBytes - kSeqStaticLds);
 }
 
-size_t lstm_bstep_lds(int M, int K, int64_t nnzT) {
-  return size_t(round_up(M + 1, 16)) * kBS * 4 + size_t(K) * 2048 * 4 + size_t(nnzT) * 4 +
-         align16(size_t(nnzT) * 2 + kSpmmSlack);
+size_t lstm_bstep_lds(int M, int K, int64_t nnzT, bool x3) {
+  return size_t(round_up(M + 1, 16)) * kBS * 4 + size_t(K) * (x3 ? 3072 : 2048) * 4 +
+         size_t(nnzT) * 4 + align16(size_t(nnzT) * 2 + kSpmmSlack);
 }
 
 bool lstm_bstep_ok(int M, int H, int K, int64_t nnzT) {
   return H == kH && M >= 1 && M <= kRB * 8 * 16 && K >= 1 && K <= 4 && nnzT >= 1 &&
-         lstm_bstep_lds(M, K, nnzT) <= size_t(kLdsBytes);
+         lstm_bstep_lds(M, K, nnzT, false) <= size_t(kLdsBytes);
 }
 
 int lstm_seq_pairs(int N, int device) {
@@ -1208,14 +1261,21 @@ hipError_t launch_lstm_bstep(int gates, int N, int M, int K, const int* trowptr,
 #ifdef CG_DEBUG
   a.ts = g_debug_ts;
 #endif
-  const size_t lds = lstm_bstep_lds(M, K, nnzT);
+  // the split-bf16 D_k contraction (CG_OPT_GEMM_X3) where its larger W image fits
+  const bool x3 = option(kOptGemmX3) != 0 && lstm_bstep_lds(M, K, nnzT, true) <= size_t(kLdsBytes);
+  const size_t lds = lstm_bstep_lds(M, K, nnzT, x3);
 #define CG_BSTEP(KK)                                                                              \
   case KK: {                                                                                      \
-    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_bstep<KK>), \
+    static hipError_t at = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_bstep<KK, false>), \
                                                hipFuncAttributeMaxDynamicSharedMemorySize,       \
                                                kLdsBytes);                                        \
+    static hipError_t atx = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lstm_bstep<KK, true>), \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                                kLdsBytes);                                       \
     if (at != hipSuccess) return at;                                                              \
-    hipLaunchKernelGGL(k_lstm_bstep<KK>, dim3(2 * N), dim3(kST), lds, s, a);                      \
+    if (atx != hipSuccess) return atx;                                                            \
+    if (x3) hipLaunchKernelGGL((k_lstm_bstep<KK, true>), dim3(2 * N), dim3(kST), lds, s, a);      \
+    else hipLaunchKernelGGL((k_lstm_bstep<KK, false>), dim3(2 * N), dim3(kST), lds, s, a);        \
     break;                                                                                        \
   }
   switch (K) {

@@ -99,8 +99,9 @@ enum {
                            (f32-accurate; not bitwise the f32 kernels) (default);
                            0: the f32-MFMA kernels                                    */
   CG_OPT_GEMM_X3 = 9,   /* 1: the streaming path's skinny row GEMMs (y = basis W and
-                           dBasis = dy W^T) with the same three-term split (f32-accurate;
-                           not bitwise the f32 kernel) (default); 0: f32 MFMA         */
+                           dBasis = dy W^T) and the gconv-LSTM BPTT step's D_k = dpre
+                           Wh_k^T with the same three-term split (f32-accurate; not
+                           bitwise the f32 kernels) (default); 0: f32 MFMA            */
   CG_OPT_COUNT = 10
 };
 
