@@ -237,6 +237,7 @@ struct FastBwdArgs {
   float* dw_slab;      // [N][FinK][Fout] per-sample dW partials, or NULL (no fused dW)
   int bord;            // basis layout, as FastFwdArgs::bord
   unsigned long long* ts;  // ablation build: phase timestamps (CG_TS), else NULL
+  int x3;              // dBasis = dy W^T on the split-bf16 matrix pipe (CG_OPT_GEMM_X3)
 };
 hipError_t launch_fast_forward(const FastGeom& g, int N, const FastFwdArgs& a, hipStream_t s);
 hipError_t launch_fast_backward(const FastGeom& g, int N, const FastBwdArgs& a, hipStream_t s);

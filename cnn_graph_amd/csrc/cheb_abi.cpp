@@ -944,6 +944,7 @@ int backward_impl(cg_plan* plan, int32_t N, int32_t Fin, int32_t K, int32_t Fout
       a.dx_acc = dx_acc;
       a.dw_slab = fused ? slabs : nullptr;
       a.bord = layout == CG_BASIS_ORDERS ? basis_mb(M) : 0;
+      a.x3 = cg::option(cg::kOptGemmX3) != 0 ? 1 : 0;
 #ifdef CG_DEBUG
       a.ts = cg::g_debug_ts;
 #endif

@@ -49,6 +49,7 @@
 #include <type_traits>
 
 #include "cg_internal.h"
+#include "split_bf16.h"
 
 namespace cg {
 namespace fastk {
@@ -684,7 +685,46 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
     }
   };
   if (!CG_DBG(A.dbg, 2)) {
-    if (fastA) {
+    if (fastA && A.x3) {
+      // the split-bf16 form (split_bf16.h): 16-deep k-blocks of f, element e
+      // of lane half h in block kb is f = h*ns + 8kb + e -- the lane's own dy
+      // registers for A, W[j][f] from LDS for B (split once, both tiles)
+      const int j = li;
+      const bool jv = j < FinK;
+      const float* wrow = s_W + imin(j, FinK - 1) * ws + h * ns;
+      const int nkb = (ns + 7) >> 3;
+      x3::Split3 wb[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (jv && 8 * kb + e < ns) ? wrow[8 * kb + e] : 0.f;
+        wb[kb] = x3::split3(v);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int mt = wave + t * kW;
+        if (mt < mtiles) {
+          const bool mv = mt * 32 + li < M;
+          f32x16 acc;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            if (kb < nkb) {
+              float v[8];
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const int f = 8 * kb + e;
+                v[e] = (mv && f < ns) ? comp(av[t][f >> 2], f & 3) : 0.f;
+              }
+              acc = x3::mfma32_x3(x3::split3(v), wb[kb], acc);
+            }
+          }
+          store_D(acc, mt, j);
+        }
+      }
+    } else if (fastA) {
       const int j = li;
       const bool jv = j < FinK;
       const float* wrow = s_W + imin(j, FinK - 1) * ws + h * ns;
