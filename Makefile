@@ -14,7 +14,7 @@ SRCS     := $(SRC_DIR)/cheb_fast.hip $(SRC_DIR)/cheb_resident.hip $(SRC_DIR)/che
 # the orders layout for Fin <= 2 only), compiled in parallel
 FAST_INST := fastf_1_1_0 fastf_1_2_0 fastf_2_1_0 fastf_2_2_0 fastf_4_1_0 fastf_4_2_0 \
              fastf_1_1_1 fastf_1_2_1 fastf_2_1_1 fastf_2_2_1 \
-             fastb_1_0 fastb_1_1 fastb_1_2 fastb_2_0 fastb_2_1 fastb_2_2 fastb_4_0 fastb_4_1
+             fastb_1_0 fastb_1_1 fastb_1_2 fastb_1_3 fastb_2_0 fastb_2_1 fastb_2_2 fastb_2_3 fastb_4_0 fastb_4_1
 OBJS     := $(patsubst $(SRC_DIR)/%,$(OBJ_DIR)/%.o,$(SRCS)) $(patsubst %,$(OBJ_DIR)/%.o,$(FAST_INST))
 DEPS     := $(OBJS:.o=.d)
 

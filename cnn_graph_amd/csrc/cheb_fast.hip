@@ -46,10 +46,12 @@ hipError_t launch_fast_forward(const FastGeom& g, int N, const FastFwdArgs& a, h
 }
 
 hipError_t launch_fast_backward(const FastGeom& g, int N, const FastBwdArgs& a, hipStream_t s) {
-  const int dw = a.dw_slab == nullptr ? 0 : (a.bord ? 2 : 1);
+  // orders-layout basis: the fused dW on the split-bf16 matrix pipe with CG_OPT_GEMM_X3
+  const int dw = a.dw_slab == nullptr ? 0 : (a.bord ? (a.x3 ? 3 : 2) : 1);
 #define CG_B(FV_)                                                                      \
   if (a.Fin == FV_)                                                                    \
-    return dw == 2 ? fastk::launch_bwd_fast_t<FV_, 2>(g.bwd_lds, N, a, s)              \
+    return dw == 3 ? fastk::launch_bwd_fast_t<FV_, 3>(g.bwd_lds, N, a, s)              \
+           : dw == 2 ? fastk::launch_bwd_fast_t<FV_, 2>(g.bwd_lds, N, a, s)            \
            : dw == 1 ? fastk::launch_bwd_fast_t<FV_, 1>(g.bwd_lds, N, a, s)            \
                      : fastk::launch_bwd_fast_t<FV_, 0>(g.bwd_lds, N, a, s);
   CG_B(1) CG_B(2)

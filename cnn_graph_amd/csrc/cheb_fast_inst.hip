@@ -1,6 +1,7 @@
 // One instantiation of the fast resident kernels (cheb_fast_kern.h), chosen
 // by the Makefile through -DCG_FAST_FWD/-DCG_FAST_BWD, -DCG_FV and
-// -DCG_NT (forward: 32-wide Fout tiles) -DCG_OB (forward: orders-layout basis) or -DCG_DW (backward: 0 no fused dW, 1 fused dW, 2 fused dW from the orders-layout basis).
+// -DCG_NT (forward: 32-wide Fout tiles) -DCG_OB (forward: orders-layout basis) or -DCG_DW (backward: 0 no fused dW, 1 fused dW, 2 fused dW from the orders-layout basis, 3 the
+// same on the split-bf16 matrix pipe).
 #include "cheb_fast_kern.h"
 
 namespace cg {

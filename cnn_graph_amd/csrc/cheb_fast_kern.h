@@ -425,14 +425,16 @@ __global__ __launch_bounds__(kT) void cheb_fwd_fast(FastFwdArgs A) {
 // ---------------------------------------------------------------------------
 // Backward: dBasis (phase A), Clenshaw over L~^T -> dx, fused dW partial
 // ---------------------------------------------------------------------------
-// DW: 0 no fused dW, 1 fused dW from the rows-layout basis, 2 from the orders layout
+// DW: 0 no fused dW, 1 fused dW from the rows-layout basis, 2 from the orders
+// layout, 3 from the orders layout on the split-bf16 matrix pipe (dw_x3_*)
 template <int FV, int DW>
 struct Bwd {
   typedef typename VecT<FV>::type V;
   static constexpr int REC = 12 * FV;
   static constexpr int NU = 2;  // dW MFMAs per recurrence step
   static constexpr int PF = 6;  // dW operand buffers: loads run PF steps ahead
-  static constexpr bool OB = DW == 2;
+  static constexpr bool OB = DW >= 2;
+  static constexpr bool X3 = DW == 3;
   static_assert(NU == 2 && PF % 2 == 0, "the orders-layout dW loads one row octet per two steps");
 
   const FastBwdArgs& A;
@@ -444,7 +446,13 @@ struct Bwd {
   int dm0, dm1, npair, nexti;
   V g1, g2;  // G_{k+1}, G_{k+2} of the own row
   f32x16 dacc;
-  float da[PF][NU], db[PF][NU];
+  float da[X3 ? 1 : PF][NU], db[X3 ? 1 : PF][NU];
+  // X3: 16-row groups, group g = octets w + 16 (2g + h) of this wave (lane
+  // half h takes 8 contiguous rows, element e = row 8 oct + e): the basis
+  // plane's 32 contiguous bytes and 8 dy rows per lane, one group in flight;
+  // consumed every 6 recurrence steps (BUF == 5)
+  float xr[8], yr[8];
+  int ngrp, oct_lim;
 
   __device__ __forceinline__ Bwd(const FastBwdArgs& a, char* smem, int tid) : A(a) {
     K = a.K;
@@ -530,6 +538,32 @@ struct Bwd {
 #pragma unroll
     for (int u = 0; u < NU; ++u) dw_mfma1(buf, i0, u);
   }
+  // X3: group g's operands into xr / yr (a group past the wave's octets loads
+  // octet 0: its values are masked in dw_x3_mfma)
+  __device__ __forceinline__ void dw_x3_load(int g) {
+    const int oct0 = wave + kW * (2 * g + h);
+    const int oct = oct0 < oct_lim ? oct0 : 0;
+    const int jc = imin(li, FinK - 1), fc = imin(li, Fout - 1);
+    const float* bp = A.basis + size_t(n) * FinK * bord + size_t(jc) * bord + 8 * oct;
+    const float4 b0 = *reinterpret_cast<const float4*>(bp);
+    const float4 b1 = *reinterpret_cast<const float4*>(bp + 4);
+    xr[0] = b0.x; xr[1] = b0.y; xr[2] = b0.z; xr[3] = b0.w;
+    xr[4] = b1.x; xr[5] = b1.y; xr[6] = b1.z; xr[7] = b1.w;
+    const float* dyn = A.dy + size_t(n) * M * Fout;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) yr[e] = dyn[size_t(imin(8 * oct + e, M - 1)) * Fout + fc];
+  }
+  // X3: the group's six bf16 MFMAs (rows >= M: the basis planes hold zeros there)
+  __device__ __forceinline__ void dw_x3_mfma(int g) {
+    const bool v = wave + kW * (2 * g + h) < oct_lim;
+    float x[8], y[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x[e] = (v && li < FinK) ? xr[e] : 0.f;
+      y[e] = (v && li < Fout) ? yr[e] : 0.f;
+    }
+    dacc = x3::mfma32_x3(x3::split3(x), x3::split3(y), dacc);
+  }
 
   template <int L, int CUR, int NX1, int NX2, int BUF>
   __device__ __forceinline__ void step(int i) {
@@ -544,12 +578,19 @@ struct Bwd {
     V gth[L > 0 ? L : 1];
     if (i >= 1) r.template gather<FV, L, NX1>(ring, gth);
     // (ablation build: bit 64 skips the dW MFMAs, bit 128 the dW loads)
-    if (DW && !CG_DBG(A.dbg, 64)) dw_mfma1(BUF, i * NU, 0);
+    if constexpr (X3) {
+      if (BUF == 5 && i / 6 < ngrp) {  // every sixth step: one group's MFMAs, the next group's loads
+        dw_x3_mfma(i / 6);
+        if (i / 6 + 1 < ngrp) dw_x3_load(i / 6 + 1);
+      }
+    } else if (DW && !CG_DBG(A.dbg, 64)) {
+      dw_mfma1(BUF, i * NU, 0);
+    }
     const float c = (k >= 1) ? 2.f : 1.f;
     V a = vzero<V>();
     if (i >= 1) a = r.template reduce<FV, L>(gth);
-    if (DW && !CG_DBG(A.dbg, 64)) dw_mfma1(BUF, i * NU, 1, &a);
-    if (DW && !CG_DBG(A.dbg, 128)) {
+    if (!X3 && DW && !CG_DBG(A.dbg, 64)) dw_mfma1(BUF, i * NU, 1, &a);
+    if (!X3 && DW && !CG_DBG(A.dbg, 128)) {
       if (!OB) {
         dw_load(BUF, (i + PF) * NU);  // refill for step i + PF
       } else if (BUF & 1) {
@@ -588,7 +629,15 @@ struct Bwd {
     r.template load<FV, L>(A.E, threadIdx.x);
     g1 = vzero<V>();
     g2 = g1;
-    if (DW) {
+    if (X3) {
+      oct_lim = (M + 7) >> 3;
+      const int no = oct_lim > wave ? (oct_lim - wave + kW - 1) / kW : 0;  // this wave's octets
+      ngrp = (no + 1) >> 1;
+      npair = 0;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dacc[e] = 0.f;
+      if (ngrp > 0) dw_x3_load(0);
+    } else if (DW) {
       if (OB) {  // row octets wave, wave + 16, ... (dw_row)
         const int no = (M + 7) >> 3;
         dm0 = 0;
@@ -787,7 +836,14 @@ __global__ __launch_bounds__(kT) void cheb_bwd_fast(FastBwdArgs A) {
   CG_TS(A.ts, 4);
 
   if (DW) {
-    // remaining row pairs (K small relative to M/32), then the cross-wave sum
+    // remaining row pairs / groups (K small relative to M/32), then the cross-wave sum
+    if constexpr (B::X3) {
+      for (int g = c.K / 6; g < c.ngrp; ++g) {
+        // (group K / 6 was loaded by the last in-loop group, or by go())
+        c.dw_x3_mfma(g);
+        if (g + 1 < c.ngrp) c.dw_x3_load(g + 1);
+      }
+    }
     for (int i0 = c.K * B::NU; i0 < c.npair; i0 += B::NU) {
       c.dw_load(0, i0);
       c.dw_mfma(0, i0);
