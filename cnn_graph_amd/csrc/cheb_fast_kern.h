@@ -540,18 +540,30 @@ struct Bwd {
   }
   // X3: group g's operands into xr / yr (a group past the wave's octets loads
   // octet 0: its values are masked in dw_x3_mfma)
+  // (buffer loads over the sample's slabs: 32-bit offsets, the bases in
+  // SGPRs; a dy row past M reads 0 -- its basis entries are 0 anyway)
   __device__ __forceinline__ void dw_x3_load(int g) {
     const int oct0 = wave + kW * (2 * g + h);
     const int oct = oct0 < oct_lim ? oct0 : 0;
-    const int jc = imin(li, FinK - 1), fc = imin(li, Fout - 1);
-    const float* bp = A.basis + size_t(n) * FinK * bord + size_t(jc) * bord + 8 * oct;
-    const float4 b0 = *reinterpret_cast<const float4*>(bp);
-    const float4 b1 = *reinterpret_cast<const float4*>(bp + 4);
-    xr[0] = b0.x; xr[1] = b0.y; xr[2] = b0.z; xr[3] = b0.w;
-    xr[4] = b1.x; xr[5] = b1.y; xr[6] = b1.z; xr[7] = b1.w;
-    const float* dyn = A.dy + size_t(n) * M * Fout;
+    int lq = threadIdx.x;  // the lane's column re-derived here (a hoisted copy is spilled)
+    asm volatile("" : "+v"(lq));
+    const int jc = imin(lq & 31, FinK - 1), fc = imin(lq & 31, Fout - 1);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(A.basis + size_t(n) * FinK * bord), 0, FinK * bord * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(A.dy + size_t(n) * M * Fout), 0, M * Fout * 4, 0x00020000);
+    const int bo = (jc * bord + 8 * oct) * 4;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) yr[e] = dyn[size_t(imin(8 * oct + e, M - 1)) * Fout + fc];
+    for (int q = 0; q < 2; ++q) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rb, bo + 16 * q, 0, 0);
+      xr[4 * q] = __uint_as_float(v[0]);
+      xr[4 * q + 1] = __uint_as_float(v[1]);
+      xr[4 * q + 2] = __uint_as_float(v[2]);
+      xr[4 * q + 3] = __uint_as_float(v[3]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      yr[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, ((8 * oct + e) * Fout + fc) * 4, 0, 0));
   }
   // X3: the group's six bf16 MFMAs (rows >= M: the basis planes hold zeros there)
   __device__ __forceinline__ void dw_x3_mfma(int g) {
@@ -562,7 +574,7 @@ struct Bwd {
       x[e] = (v && li < FinK) ? xr[e] : 0.f;
       y[e] = (v && li < Fout) ? yr[e] : 0.f;
     }
-    dacc = x3::mfma32_x3(x3::split3(x), x3::split3(y), dacc);
+    dacc = x3::mfma32_x3b(x3::split3(x), y, dacc);
   }
 
   template <int L, int CUR, int NX1, int NX2, int BUF>

@@ -62,6 +62,36 @@ __device__ __forceinline__ f32x16 mfma32_x3(const Split3& a, const Split3& b, f3
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, b.hi, c, 0, 0, 0);
 }
 
+// c += a * b with b given as 8 raw f32 values, split one term at a time (a
+// tighter register peak than split3(b): one B fragment live at once); the same
+// six products, in the order lo*hi, mid*hi, hi*hi, mid*mid, hi*mid, hi*lo
+__device__ __forceinline__ f32x16 mfma32_x3b(const Split3& a, const float (&b)[8], f32x16 c) {
+  float r[8];
+  u32x4 w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = __builtin_amdgcn_perm(__float_as_uint(b[2 * i + 1]), __float_as_uint(b[2 * i]), 0x07060302u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = b[j] - __uint_as_float(__float_as_uint(b[j]) & 0xffff0000u);
+  bf16x8 f = __builtin_bit_cast(bf16x8, w);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.lo, f, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, f, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, f, c, 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = __builtin_amdgcn_perm(__float_as_uint(r[2 * i + 1]), __float_as_uint(r[2 * i]), 0x07060302u);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = r[j] - __uint_as_float(__float_as_uint(r[j]) & 0xffff0000u);
+  f = __builtin_bit_cast(bf16x8, w);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.mid, f, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, f, c, 0, 0, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = __builtin_amdgcn_perm(__float_as_uint(r[2 * i + 1]), __float_as_uint(r[2 * i]), 0x07060302u);
+  f = __builtin_bit_cast(bf16x8, w);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.hi, f, c, 0, 0, 0);
+}
+
 // c += a * b over one 32-deep k-block of a 16x16 tile
 __device__ __forceinline__ f32x4 mfma16_x3(const Split3& a, const Split3& b, f32x4 c) {
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.mid, b.mid, c, 0, 0, 0);
