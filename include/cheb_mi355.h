@@ -98,10 +98,11 @@ enum {
                            into three bf16 terms, six products accumulated in f32
                            (f32-accurate; not bitwise the f32 kernels) (default);
                            0: the f32-MFMA kernels                                    */
-  CG_OPT_GEMM_X3 = 9,   /* 1: the streaming path's skinny row GEMMs (y = basis W and
-                           dBasis = dy W^T) and the gconv-LSTM BPTT step's D_k = dpre
-                           Wh_k^T with the same three-term split (f32-accurate; not
-                           bitwise the f32 kernels) (default); 0: f32 MFMA            */
+  CG_OPT_GEMM_X3 = 9,   /* 1: the same three-term split for the fast backward's dBasis
+                           and fused dW (config B), the streaming path's skinny row
+                           GEMMs (y = basis W, dBasis = dy W^T) and the gconv-LSTM BPTT
+                           step's D_k = dpre Wh_k^T (f32-accurate; not bitwise the f32
+                           kernels) (default); 0: f32 MFMA                            */
   CG_OPT_COUNT = 10
 };
 

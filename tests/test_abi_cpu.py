@@ -34,10 +34,10 @@ def test_release_library_refuses_ablation_only_options(built_lib):
     and does not contain their kernels."""
     h = _lib.lib()
     for name, v in (("dw_direct", 2), ("dw_direct", 3), ("dw_w2", 0), ("spmm_pw", 0), ("grp_pc", 0),
-                    ("clen_dy", 0), ("clen_dy", 2), ("dw_x3", 2)):
+                    ("clen_dy", 0), ("clen_dy", 2), ("dw_x3", 2), ("gemm_x3", 2)):
         assert h.cg_set_option(_lib.OPTIONS[name], v) == _lib.CG_ERR_ARG, (name, v)
     for name, v in (("dw_direct", 0), ("dw_direct", 1), ("dw_w2", 1), ("spmm_pw", 1), ("grp_pc", 1),
-                    ("clen_dy", 1), ("dw_x3", 0), ("dw_x3", 1)):
+                    ("clen_dy", 1), ("dw_x3", 0), ("dw_x3", 1), ("gemm_x3", 0), ("gemm_x3", 1)):
         assert h.cg_set_option(_lib.OPTIONS[name], v) == _lib.CG_OK, (name, v)
     with open(_lib.LIB_PATH, "rb") as f:
         blob = f.read()
