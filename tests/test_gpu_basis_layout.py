@@ -347,3 +347,42 @@ def test_planes_input_in_plane0_bitwise(dev, variant, gname, N, Fin, K, Fout):
     assert torch.equal(ra.y, rb.y)
     assert torch.equal(ra.dx, rb.dx)
     assert torch.equal(ra.dW, rb.dW)
+
+
+@pytest.mark.parametrize("layout", ["orders", "rows"])
+def test_fast_backward_x3_vs_f32(dev, cg_opts, layout):
+    """The fast backward's split-bf16 dBasis (and, orders layout, fused dW:
+    cheb_bwd_fast<FV, 3>) against its f32-MFMA form (CG_OPT_GEMM_X3 = 0) on
+    config B's shape at the bench batch: dx and dW agree to f32 rounding
+    (1e-6 normwise) and both sit within 1e-5 of the float64 oracle on a
+    64-sample slice; the forward is untouched (basis and y bitwise)."""
+    from cnn_graph_amd import ops
+    c = case(load_golden("golden_B.npz"))
+    M, N, Fin, K, Fout = c["M"], 256, 1, 25, 32
+    plan = _plan(c)
+    g = torch.Generator().manual_seed(77)
+    x = torch.rand((N, M, Fin), generator=g).to(dev)
+    W = (torch.randn((Fin * K, Fout), generator=g) * 0.1).to(dev)
+    dy = torch.randn((N, M, Fout), generator=g).to(dev)
+    out = {}
+    for x3 in (0, 1):
+        cg_opts("gemm_x3", x3)
+        r = ops.ChebRunner(plan, N, Fin, K, Fout, dev, basis_layout=layout)
+        r.forward(x, W)
+        r.backward(dy, W)
+        torch.cuda.synchronize()
+        out[x3] = (r.basis.clone(), r.y.clone(), r.dx.clone(), r.dW.clone())
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    for i in (2, 3):
+        err = O.normwise_err(out[1][i].cpu().double().numpy(), out[0][i].cpu().double().numpy())
+        assert err < 1e-6, (i, err)
+    rp, ci, va = c["Lt_rowptr"], c["Lt_col"], c["Lt_val"]
+    n = 64
+    xs, Ws, dys = x[:n].cpu().numpy(), W.cpu().numpy(), dy[:n].cpu().numpy()
+    basis, _ = O.cheb_forward(xs, rp, ci, va, Ws, K)
+    dx64, _ = O.cheb_backward(dys, basis, Ws, rp, ci, va, n, M, Fin, K)
+    basis_all, _ = O.cheb_forward(x.cpu().numpy(), rp, ci, va, Ws, K)
+    _, dW64 = O.cheb_backward(dy.cpu().numpy(), basis_all, Ws, rp, ci, va, N, M, Fin, K)
+    for x3 in (0, 1):
+        assert O.normwise_err(out[x3][2][:n].cpu().double().numpy(), dx64) < 1e-5
+        assert O.normwise_err(out[x3][3].cpu().double().numpy(), dW64) < 1e-5
