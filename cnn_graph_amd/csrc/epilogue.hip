@@ -55,14 +55,40 @@ __device__ __forceinline__ float drop_u(unsigned long long seed, int64_t i) {
 }
 
 // bwd = 0: y = (x / keep) * floor(keep + u);  bwd = 1: y = (x * floor(keep + u)) / keep
+__device__ __forceinline__ float drop_one(float x, float keep, unsigned long long seed, int64_t i,
+                                          int bwd) {
+#pragma clang fp contract(off)
+  const float b = floorf(keep + drop_u(seed, i));
+  return bwd ? (x * b) / keep : (x / keep) * b;
+}
+
 __global__ __launch_bounds__(256) void k_dropout(const float* __restrict__ x, float* __restrict__ y,
                                                  int64_t n, float keep, unsigned long long seed,
                                                  int bwd) {
-#pragma clang fp contract(off)
-  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
-    const float b = floorf(keep + drop_u(seed, i));
-    y[i] = bwd ? (x[i] * b) / keep : (x[i] / keep) * b;
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256)
+    y[i] = drop_one(x[i], keep, seed, i, bwd);
+}
+
+// 16-byte aligned x / y: four elements per thread (one dwordx4 load and
+// store; the same per-element draw and arithmetic, so the same bits), the
+// n % 4 tail by the first threads
+__global__ __launch_bounds__(256) void k_dropout4(const float4* __restrict__ x, float4* __restrict__ y,
+                                                  int64_t n, float keep, unsigned long long seed,
+                                                  int bwd) {
+  const int64_t n4 = n >> 2;
+  for (int64_t q = int64_t(blockIdx.x) * 256 + threadIdx.x; q < n4; q += int64_t(gridDim.x) * 256) {
+    const float4 v = x[q];
+    float4 o;
+    o.x = drop_one(v.x, keep, seed, 4 * q, bwd);
+    o.y = drop_one(v.y, keep, seed, 4 * q + 1, bwd);
+    o.z = drop_one(v.z, keep, seed, 4 * q + 2, bwd);
+    o.w = drop_one(v.w, keep, seed, 4 * q + 3, bwd);
+    y[q] = o;
   }
+  const int64_t t = 4 * n4 + int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (t < n)
+    reinterpret_cast<float*>(y)[t] =
+        drop_one(reinterpret_cast<const float*>(x)[t], keep, seed, t, bwd);
 }
 
 // one workgroup: t <- (t * c) / max(sqrt(sum t^2), c) in place (the norm's sum
@@ -337,6 +363,12 @@ hipError_t launch_stack_merge_bwd(const float* dy, const float* o, const float* 
 
 hipError_t launch_dropout(const float* x, float* y, int64_t n, float keep, unsigned long long seed,
                           int bwd, hipStream_t s) {
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0 && n >= 4) {
+    hipLaunchKernelGGL(k_dropout4, dim3(grid1d((n + 3) / 4, 256)), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), n, keep,
+                       seed, bwd);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_dropout, dim3(grid1d(n, 256)), dim3(256), 0, s, x, y, n, keep, seed, bwd);
   return hipGetLastError();
 }

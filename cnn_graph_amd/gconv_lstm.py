@@ -316,10 +316,14 @@ class _Layer(torch.autograd.Function):
         ctx.save_for_backward(basis_x, planes if fused else basis_h, Wx, Wh, act, cs, c0, h0, hs)
         ctx.cell, ctx.zero_init, ctx.shape, ctx.fused = cell, zero_init, (T, N, M, F), fused
         ctx.seq_x = seq_x
-        return hs, cs[T - 1].clone()
+        # outputs nobody differentiates reach the backward as None (no zero
+        # [T, N, M, H] gradient materialised for a sequence read only at its
+        # last step: h_T is an output of its own)
+        ctx.set_materialize_grads(False)
+        return hs, cs[T - 1].clone(), hs[T - 1].clone()
 
     @staticmethod
-    def backward(ctx, dhs, dcT):
+    def backward(ctx, dhs, dcT, dhT):
         basis_x, hb, Wx, Wh, act, cs, c0, h0, hs = ctx.saved_tensors
         cell, zero_init, fused = ctx.cell, ctx.zero_init, ctx.fused
         H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
@@ -333,12 +337,21 @@ class _Layer(torch.autograd.Function):
         dpre = torch.empty((T, R, 4 * H), device=dev, dtype=torch.float32)
         dhs = dhs.contiguous() if dhs is not None else None
         dc = dcT.contiguous() if dcT is not None else None
+        dh_last = None  # the gradient of h_{T-1}: through hs and through h_T
+        if dhT is not None:
+            dh_last = dhT.contiguous() if dhs is None else dhs[T - 1] + dhT
+        elif dhs is not None:
+            dh_last = dhs[T - 1]
+
+        def dh_at(t):
+            return dh_last if t == T - 1 else (None if dhs is None else dhs[t])
+
         dh_rec = None
         t_first = 1 if zero_init else 0  # first step whose h-conv ran
         for t in range(T - 1, -1, -1):
             c_prev = (None if zero_init else c0) if t == 0 else cs[t - 1]
             if cell.seq and t < t_first:  # no h-conv at this step: pointwise only, act as stored
-                _, dc, _ = ops.lstm_bwd_step(plan, None if dhs is None else dhs[t], dh_rec, dc,
+                _, dc, _ = ops.lstm_bwd_step(plan, dh_at(t), dh_rec, dc,
                                              act[t], c_prev, cs[t], Wh, K, gates, out_dpre=dpre[t],
                                              act_unit_major=True, need_dh_prev=False)
                 dh_rec = None
@@ -346,14 +359,14 @@ class _Layer(torch.autograd.Function):
             if cell.seq and t >= t_first:
                 # one launch: gates backward, dBasis = dpre Wh^T on MFMA and the
                 # reverse recurrence over L~^T -> the gradient of h_{t-1}
-                _, dc, dh_rec = ops.lstm_bwd_step(plan, None if dhs is None else dhs[t], dh_rec,
+                _, dc, dh_rec = ops.lstm_bwd_step(plan, dh_at(t), dh_rec,
                                                   dc, act[t], c_prev, cs[t], Wh, K, gates,
                                                   out_dpre=dpre[t], act_unit_major=True)
                 continue
             # the sequence kernel's act records are unit-major: gate-major for the
             # pointwise kernel (step 0 of a zero-state layer only)
             act_t = act[t].view(R, H, 4).transpose(1, 2).reshape(R, 4 * H) if cell.seq else act[t]
-            dpre_t, dc = ops.lstm_cell_backward(None if dhs is None else dhs[t], dh_rec, dc, act_t,
+            dpre_t, dc = ops.lstm_cell_backward(dh_at(t), dh_rec, dc, act_t,
                                                 c_prev, cs[t], H, gates, out_dpre=dpre[t])
             if t >= t_first:
                 dh_rec, _ = ops.cheb_backward(plan, dpre[t].view(N, M, 4 * H),
@@ -460,12 +473,12 @@ def layer(cell, xs: torch.Tensor, initial_state=None):
     check_now = not (torch.is_grad_enabled() and any(t.requires_grad for t in ins))
     if initial_state is None:
         z = xs.new_zeros(())
-        hs, cT = _Layer.apply(xs, z, z, cell.Wx, cell.Wh, cell.b, cell, True, check_now)
+        hs, cT, hT = _Layer.apply(xs, z, z, cell.Wx, cell.Wh, cell.b, cell, True, check_now)
     else:
         c0, h0 = initial_state
-        hs, cT = _Layer.apply(xs, c0.contiguous(), h0.contiguous(), cell.Wx, cell.Wh, cell.b, cell,
-                              False, check_now)
-    return hs, LSTMStateTuple(cT, hs[-1])
+        hs, cT, hT = _Layer.apply(xs, c0.contiguous(), h0.contiguous(), cell.Wx, cell.Wh, cell.b,
+                                  cell, False, check_now)
+    return hs, LSTMStateTuple(cT, hT)
 
 
 def static_rnn(cells, inputs, initial_states=None):
@@ -640,9 +653,27 @@ class GLSTMModel:
         return x.contiguous()
 
     def forward(self, x):
-        """inference_glstm: the fc layer's output [N, M, out_features]."""
-        outs, _ = static_rnn(self.wrapped, self._steps(x))
-        return ops.cheb_conv(outs[-1].contiguous(), self.W_fc, self.plan, self.K)
+        """inference_glstm: the fc layer's output [N, M, out_features].
+
+        static_rnn(self.wrapped, ...) then outputs[-1], with the last layer's
+        sequence read at its last step only: that layer runs unwrapped, its
+        h_T (a separate output: the backward gets no zero [T, N, M, H]
+        gradient) goes through the dropout as the last-step slice of the
+        layer's mask (same seed, element offset (T-1)*N*M*H) -- the values
+        and gradients of the whole-sequence form, 1/T of its dropout traffic."""
+        xs = self._steps(x)
+        last = len(self.wrapped) - 1
+        for li, cell in enumerate(self.wrapped):
+            if li < last:
+                xs, _ = layer(cell, xs)
+                continue
+            drop = isinstance(cell, DropoutWrapper)
+            _, st = layer(cell.cell if drop else cell, xs)
+            h = st.h
+            if drop:
+                h = ops.dropout(h, cell.output_keep_prob, cell.next_seed(),
+                                offset=(xs.shape[0] - 1) * h.numel())
+        return ops.cheb_conv(h, self.W_fc, self.plan, self.K)
 
     def train_step(self, x, labels, stream=None):
         """One optimizer step; returns the device loss [1] (this rank's batch)."""

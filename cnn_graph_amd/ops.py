@@ -844,12 +844,21 @@ class _Dropout(torch.autograd.Function):
         return dx, None, None
 
 
-def dropout(x, keep_prob: float, seed: int):
+DROP_WEYL = 0x9E3779B97F4A7C15  # the mask draw's Weyl increment (epilogue.hip drop_u)
+
+
+def dropout(x, keep_prob: float, seed: int, offset: int = 0):
     """y = (x / keep_prob) * floor(keep_prob + u), u ~ U[0,1) per element from
-    (seed, index); keep_prob == 1 returns x."""
+    (seed, index); keep_prob == 1 returns x.
+
+    offset: x is the slice starting at element ``offset`` of a larger tensor
+    dropped out under ``seed`` -- element i draws as element offset + i would
+    there (the draw hashes seed + DROP_WEYL * (index + 1), so the offset folds
+    into the seed: the same mask bits, no wider ABI)."""
     if keep_prob >= 1.0:
         return x
-    return _Dropout.apply(x, keep_prob, int(seed) & ((1 << 64) - 1))
+    s = (int(seed) + DROP_WEYL * int(offset)) & ((1 << 64) - 1)
+    return _Dropout.apply(x, keep_prob, s)
 
 
 def clip_by_norm_(grads, clip_norm: float, check_numerics: bool = True):

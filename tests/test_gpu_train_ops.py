@@ -93,6 +93,65 @@ def test_dropout_wrapper_layer_outputs_only(dev):
     assert torch.equal(states[1].h, h2[-1])
 
 
+def test_dropout_vector_and_offset_slices(dev):
+    """The four-per-thread kernel (16-byte aligned x / y) and the scalar one
+    (misaligned) draw the same bits; a slice dropped with offset = its first
+    element's index equals that slice of the whole tensor's dropout, forward
+    and backward (GLSTMModel drops only the last step of its last layer this
+    way)."""
+    from cnn_graph_amd import ops
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    n, keep, seed = 100003, 0.8, 0xFEEDFACECAFEBEEF
+    x = torch.randn((n,), device=dev, generator=g)
+    y = ops.dropout(x, keep, seed)
+    buf = torch.empty((n + 1,), device=dev)
+    buf[1:].copy_(x)  # 4-byte offset: the scalar kernel
+    assert torch.equal(ops.dropout(buf[1:], keep, seed), y)
+    for off, m in ((0, 7), (4, 4096), (13, 1001), (n - 5, 5), (64 * 1024, 30000)):
+        xs = x[off:off + m].clone().requires_grad_()
+        ys = ops.dropout(xs, keep, seed, offset=off)
+        assert torch.equal(ys, y[off:off + m]), off
+        dy = torch.randn((m,), device=dev, generator=g)
+        ys.backward(dy)
+        full = x.clone().requires_grad_()
+        dfull = torch.zeros((n,), device=dev)
+        dfull[off:off + m] = dy
+        ops.dropout(full, keep, seed).backward(dfull)
+        assert torch.equal(xs.grad, full.grad[off:off + m]), off
+
+
+def test_glstm_forward_last_step_equals_static_rnn(dev):
+    """GLSTMModel.forward reads the last layer at its last step only (h_T as
+    its own output, the dropout on that slice with the mask offset): output
+    and every gradient equal the whole-sequence form static_rnn(wrapped) +
+    outputs[-1] (lib/gconv_lstm.py:625-636), bitwise, for 1 and 2 layers."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__)))
+    import glstm_dp_worker as Wk
+    from cnn_graph_amd import ops
+    from cnn_graph_amd.gconv_lstm import GLSTMModel, static_rnn
+    L, x, labels = Wk.problem()
+    xs = torch.from_numpy(x[:2]).to(dev)
+    for layers in (1, 2):
+        ms = [GLSTMModel(L, 2, Wk.T, Wk.FIN, num_hidden=Wk.H, K=Wk.K, out_features=Wk.FOUT,
+                         layer_count=layers, keep_prob=0.8, device=dev, seed=21) for _ in range(2)]
+        a, b = ms
+        ya = a.forward(xs)
+        outs, _ = static_rnn(b.wrapped, b._steps(xs))
+        yb = ops.cheb_conv(outs[-1].contiguous(), b.W_fc, b.plan, b.K)
+        assert torch.equal(ya, yb), layers
+        dy = torch.randn(ya.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+        a.grad.zero_()
+        b.grad.zero_()
+        ya.backward(dy)
+        yb.backward(dy)
+        torch.cuda.synchronize()
+        assert a.grad.abs().sum() > 0
+        assert torch.equal(a.grad, b.grad), (layers, float((a.grad - b.grad).abs().max()))
+
+
 def test_clip_by_norm_and_check_numerics(dev):
     from cnn_graph_amd import ops
     rng = np.random.default_rng(4)
