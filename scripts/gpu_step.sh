@@ -1,16 +1,21 @@
 #!/bin/bash
-# Scratch GPU step (rewritten per experiment): LSTM / dropout tests, then the
-# config E bench and its kernel trace.
+# Scratch GPU step (rewritten per experiment): config E new library vs
+# $OLD (CG_LIB_PATH), then the LSTM tests (no -x: the list of what differs).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-step}
+OLD=$GRAFT_REPO_ROOT/cnn_graph_amd/libcheb_old.so
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_train_ops.py tests/test_gpu_lstm.py tests/test_gpu_glstm_dp.py -x -q --timeout 300 --timeout-method thread > $OUT/pytest.txt 2>&1; rc=$?
-tail -3 $OUT/pytest.txt; [ $rc = 0 ] || exit 1
 for i in 1 2; do
-timeout -k 10 300 python bench.py --config E --no-cpu-baseline > $OUT/E.$i.json 2>$OUT/E.err || { tail -20 $OUT/E.err; exit 1; }
-python3 -c "import json;d=json.load(open('$OUT/E.$i.json'));print('E', d['value'], d['ms_per_step'])"
+for v in new old; do
+if [ $v = old ]; then export CG_LIB_PATH=$OLD; else unset CG_LIB_PATH; fi
+timeout -k 10 300 python bench.py --config E --no-cpu-baseline > $OUT/E.$v.$i.json 2>$OUT/E.err || { tail -20 $OUT/E.err; exit 1; }
+timeout -k 10 300 python scripts/bench_configs.py E > $OUT/L.$v.$i.json 2>$OUT/L.err || { tail -20 $OUT/L.err; exit 1; }
+python3 -c "import json;d=json.load(open('$OUT/E.$v.$i.json'));print('$v E', d['value'], d['ms_per_step'])"
+tail -1 $OUT/L.$v.$i.json
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o E -- python3 bench.py --config E --steps 12 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1 || exit 1
-find $OUT/prof -name "*kernel_stats.csv" | head -1
+done
+unset CG_LIB_PATH
+timeout -k 10 600 python -u -m pytest tests/test_gpu_lstm.py -q --timeout 300 --timeout-method thread > $OUT/pytest.txt 2>&1; echo "pytest rc=$?"
+tail -15 $OUT/pytest.txt
