@@ -249,7 +249,7 @@ class _Layer(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xs, c0, h0, Wx, Wh, b, cell: GConvLSTMCell, zero_init: bool,
-                check_now: bool):
+                check_now: bool, want_c: bool = True):
         H, K, plan, gates = cell._num_units, cell._K, cell.plan, cell.gates
         xs = xs.contiguous()
         T, N, M, F = xs.shape
@@ -320,7 +320,8 @@ class _Layer(torch.autograd.Function):
         # [T, N, M, H] gradient materialised for a sequence read only at its
         # last step: h_T is an output of its own)
         ctx.set_materialize_grads(False)
-        return hs, cs[T - 1].clone(), hs[T - 1].clone()
+        cT = cs[T - 1].clone() if want_c else cs.new_empty(0)  # (a 16 MB copy nobody reads)
+        return hs, cT, hs[T - 1].clone()
 
     @staticmethod
     def backward(ctx, dhs, dcT, dhT):
@@ -388,7 +389,7 @@ class _Layer(torch.autograd.Function):
             if cell.seq:  # raises CGError if the forward's launch lost a pair hand-off
                 ops.lstm_seq_fault(plan, wait=True)
             return (dx_out, None if zero_init else dc, None if zero_init else dh_rec, dWx, dWh, db,
-                    None, None, None)
+                    None, None, None, None)
         if T <= t_first:
             dWh = torch.zeros_like(Wh)
         elif cell.seq:  # one GEMM over the K planes of every step with an h-conv
@@ -414,7 +415,7 @@ class _Layer(torch.autograd.Function):
         dh0 = None if zero_init else dh_rec
         if cell.seq:  # raises CGError if the forward's launch lost a pair hand-off
             ops.lstm_seq_fault(plan, wait=True)
-        return dx_out, dc0, dh0, dWx, dWh, db, None, None, None
+        return dx_out, dc0, dh0, dWx, dWh, db, None, None, None, None
 
 
 class DropoutWrapper:
@@ -455,9 +456,10 @@ class DropoutWrapper:
         return ops.dropout(out, self.output_keep_prob, self.next_seed()), new_state
 
 
-def layer(cell, xs: torch.Tensor, initial_state=None):
+def layer(cell, xs: torch.Tensor, initial_state=None, final_c: bool = True):
     """Run ``cell`` over xs [T, N, M, feat_in]; returns (hs [T, N, M, H],
-    LSTMStateTuple(c_T, h_T)).  initial_state None = zero state.
+    LSTMStateTuple(c_T, h_T)).  initial_state None = zero state; final_c False
+    = the caller does not read c_T (an empty tensor in its place, no copy).
 
     On the one-launch path a lost pair hand-off (cg_lstm_seq_fault) raises
     CGError: here when no gradient will be taken (the outputs go straight to
@@ -467,17 +469,18 @@ def layer(cell, xs: torch.Tensor, initial_state=None):
     ``cell`` may be a DropoutWrapper: the returned outputs are then dropped
     out, the state (c_T, h_T) is not (DropoutWrapper semantics)."""
     if isinstance(cell, DropoutWrapper):
-        hs, state = layer(cell.cell, xs, initial_state)
+        hs, state = layer(cell.cell, xs, initial_state, final_c)
         return ops.dropout(hs, cell.output_keep_prob, cell.next_seed()), state
     ins = [xs, cell.Wx, cell.Wh, cell.b] + ([] if initial_state is None else list(initial_state))
     check_now = not (torch.is_grad_enabled() and any(t.requires_grad for t in ins))
     if initial_state is None:
-        z = xs.new_zeros(())
-        hs, cT, hT = _Layer.apply(xs, z, z, cell.Wx, cell.Wh, cell.b, cell, True, check_now)
+        z = xs.new_empty(0)  # placeholders: a zero state is never read (no fill launch)
+        hs, cT, hT = _Layer.apply(xs, z, z, cell.Wx, cell.Wh, cell.b, cell, True, check_now,
+                                  final_c)
     else:
         c0, h0 = initial_state
         hs, cT, hT = _Layer.apply(xs, c0.contiguous(), h0.contiguous(), cell.Wx, cell.Wh, cell.b,
-                                  cell, False, check_now)
+                                  cell, False, check_now, final_c)
     return hs, LSTMStateTuple(cT, hT)
 
 
@@ -665,10 +668,10 @@ class GLSTMModel:
         last = len(self.wrapped) - 1
         for li, cell in enumerate(self.wrapped):
             if li < last:
-                xs, _ = layer(cell, xs)
+                xs, _ = layer(cell, xs, final_c=False)
                 continue
             drop = isinstance(cell, DropoutWrapper)
-            _, st = layer(cell.cell if drop else cell, xs)
+            _, st = layer(cell.cell if drop else cell, xs, final_c=False)
             h = st.h
             if drop:
                 h = ops.dropout(h, cell.output_keep_prob, cell.next_seed(),
