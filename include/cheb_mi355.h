@@ -460,7 +460,11 @@ int cg_lstm_bwd_step(cg_plan* plan, int32_t N, int32_t H, int32_t K, int32_t gat
  *   tf.nn.dropout: y = (x / keep) * floor(keep + u), u ~ U[0,1) drawn from a
  *   counter hash of (seed, element index) -- the backward regenerates the mask
  *   from the same seed: dx = (dy * floor(keep + u)) / keep.  (TF's random
- *   stream itself is not reproducible here; the semantics are.)
+ *   stream itself is not reproducible here; the semantics are.)  Element i
+ *   draws from the splitmix64 finaliser of seed + 0x9E3779B97F4A7C15 * (i + 1)
+ *   (mod 2^64), so the slice starting at element o of a tensor dropped under
+ *   seed s is dropped identically as its own tensor under seed
+ *   s + 0x9E3779B97F4A7C15 * o (GLSTMModel drops only the last step this way).
  * cg_clip_by_norm: tf.clip_by_norm(t, clip_norm) then tf.check_numerics of
  *   gconvRNN.Model._build_optim (lib/gconvRNN.py:392-402), in place on one
  *   gradient tensor: t = (t * clip_norm) / max(||t||_2, clip_norm), the norm a
