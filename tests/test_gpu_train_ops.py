@@ -93,6 +93,21 @@ def test_dropout_wrapper_layer_outputs_only(dev):
     assert torch.equal(states[1].h, h2[-1])
 
 
+def test_dropout_mask_matches_host_restatement(dev):
+    """The kernel's mask is floor(keep + u) with u the host restatement of the
+    draw (tests/test_dropout_cpu.py), element for element, both kernels."""
+    from cnn_graph_amd import ops
+    from test_dropout_cpu import draws
+    n, keep, seed = 50001, 0.8, 0x0123456789ABCDEF
+    u = draws(seed, n)
+    ref = np.floor(np.float32(keep) + u)
+    ones = torch.ones((n + 1,), device=dev)
+    got4 = (ops.dropout(ones[:n], keep, seed) != 0).cpu().numpy()  # aligned: k_dropout4
+    got1 = (ops.dropout(ones[1:], keep, seed) != 0).cpu().numpy()  # misaligned: k_dropout
+    assert np.array_equal(got4, ref != 0)
+    assert np.array_equal(got1, ref != 0)
+
+
 def test_dropout_vector_and_offset_slices(dev):
     """The four-per-thread kernel (16-byte aligned x / y) and the scalar one
     (misaligned) draw the same bits; a slice dropped with offset = its first
