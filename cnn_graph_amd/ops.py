@@ -855,6 +855,8 @@ def dropout(x, keep_prob: float, seed: int, offset: int = 0):
     dropped out under ``seed`` -- element i draws as element offset + i would
     there (the draw hashes seed + DROP_WEYL * (index + 1), so the offset folds
     into the seed: the same mask bits, no wider ABI)."""
+    if int(offset) < 0:
+        raise ValueError("dropout offset must be >= 0")
     if keep_prob >= 1.0:
         return x
     s = (int(seed) + DROP_WEYL * int(offset)) & ((1 << 64) - 1)

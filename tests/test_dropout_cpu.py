@@ -36,3 +36,10 @@ def test_keep_rate_and_range():
     kept = np.floor(keep + u).sum()
     n = u.size
     assert abs(kept - 0.8 * n) < 6 * np.sqrt(n * 0.8 * 0.2)
+
+
+def test_negative_offset_refused():
+    import pytest
+    from cnn_graph_amd import ops
+    with pytest.raises(ValueError):
+        ops.dropout(None, 0.8, 1, offset=-1)
